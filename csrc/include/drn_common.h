@@ -1,0 +1,69 @@
+// drn_common.h — shared device helpers for the gfx950 (CDNA4) kernel library.
+//
+// Storage conventions used across every kernel in csrc/kernels/:
+//   * activations are NHWC bf16 (raw uint16 storage, round-to-nearest-even on store);
+//   * conv weights are KRSC bf16 ([Cout][R][S][Cin]) so the GEMM reduction dim is contiguous;
+//   * statistics, master weights, momentum and gradients are fp32.
+// Wave width is 64 everywhere (CDNA wavefront), never 32.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define DRN_API extern "C" __attribute__((visibility("default")))
+
+typedef uint16_t bf16_t;
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+namespace drn {
+
+__device__ __forceinline__ float bf2f(uint32_t u16) { return __uint_as_float(u16 << 16); }
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  // hipcc lowers this to v_cvt_pk_bf16_f32 (RNE, NaN-preserving) on gfx950.
+  __hip_bfloat16 h = __float2bfloat16(f);
+  return __builtin_bit_cast(uint16_t, h);
+}
+
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// 8 bf16 held in a uint4 (16 bytes) <-> 8 floats.
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = pack2bf(f[0], f[1]); v.y = pack2bf(f[2], f[3]);
+  v.z = pack2bf(f[4], f[5]); v.w = pack2bf(f[6], f[7]);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// XCD-aware bijective remap of a linear workgroup id: consecutive logical tiles land on the
+// same XCD (blocks b, b+8, b+16 ... share an XCD under round-robin dispatch), so neighbouring
+// tiles that share an operand panel share that XCD's L2. Speed only, never correctness.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (bid >> 3);
+}
+
+}  // namespace drn
+
+#define DRN_RET_LAST_ERR() return (int)hipGetLastError()

@@ -1,0 +1,47 @@
+// drn_conv.h — argument blocks for the implicit-GEMM convolution kernels.
+//
+// These are plain-old-data structs so that the Python runtime can build them once per layer
+// at plan time (ctypes mirror in distributed_resnet_tensorflow_amd/ops/hip.py) and pass a
+// pointer per launch; the field order here and there must match exactly.
+#pragma once
+#include <stdint.h>
+
+// Magic-number unsigned division (n < 2^31): q = (umulhi(n, m) + n) >> s.
+struct DrnFastDiv {
+  uint32_t d, m, s, pad_;
+};
+
+// y[N][P][Q][K] = conv(x[N][H][W][C], w[K][R][S][C])  (NHWC / KRSC, bf16, fp32 accumulate)
+//
+// The same kernel runs the data-gradient of a convolution as a forward convolution of dY with
+// the flipped, channel-transposed weights; `dil` = 2 selects the zero-dilated ("transposed")
+// input indexing used for the gradient of a stride-2 convolution.
+struct DrnConvFwdArgs {
+  const void* x;          // bf16 [N][H][W][C]
+  const void* w;          // bf16 [K][R][S][C]
+  void* y;                // bf16 [N][P][Q][K]
+  const float* in_scale;  // optional [C]: fused BN apply on the input: relu(x*scale+shift)
+  const float* in_shift;  // optional [C]
+  const void* residual;   // optional bf16 [N][P][Q][K]: y = conv + residual
+  float* stats;           // optional [tiles_p][2][K]: per-pixel-tile partial sum / sumsq of y
+  int32_t N, H, W, C, K, R, S, P, Q;
+  int32_t stride, pad_h, pad_w, dil;
+  int32_t relu_in;        // 1: relu after the fused scale/shift
+  int32_t tiles_p;        // out: number of pixel tiles (rows of `stats`), filled by the host
+};
+
+// dW[K][R][S][C] (+)= sum_{n,p,q} dy[n,p,q,k] * x[n, p*st-pad+r, q*st-pad+s, c]
+// Split-K over output pixels: partial slabs out[split][K][R*S*C] (fp32); splits==1 writes
+// the final gradient directly.
+struct DrnConvWgradArgs {
+  const void* x;          // bf16 [N][H][W][C] (forward input, pre-activation if fused)
+  const void* dy;         // bf16 [N][P][Q][K]
+  float* out;             // fp32 [splits][K][R*S*C]
+  const float* in_scale;  // optional fused BN apply (recompute of the forward prologue)
+  const float* in_shift;
+  int32_t N, H, W, C, K, R, S, P, Q;
+  int32_t stride, pad_h, pad_w;
+  int32_t relu_in;
+  int32_t splits, pix_per_split;
+  DrnFastDiv fd_pq, fd_q;
+};

@@ -1,0 +1,316 @@
+// bn.hip — training-mode BatchNorm (+ReLU) for NHWC bf16 activations on gfx950.
+//
+// Replaces the cuDNN FusedBatchNorm / FusedBatchNormGrad + Relu pair of every
+// `batch_norm_relu` (reference resnet_model_official.py:41-50: momentum 0.997, eps 1e-5,
+// center+scale, per-replica statistics, moving averages via UPDATE_OPS, resnet_model.py:119).
+//
+// Statistics flow (all deterministic, no float atomics):
+//   forward  : partial sums  -> drn_bn_finalize -> scale/shift (+ running stats update)
+//              partial sums come either from drn_bn_stats or straight from the producing
+//              convolution's epilogue (conv_fwd.hip `stats`), in the same [G][2][C] layout;
+//              scale/shift are then applied inside the CONSUMER conv's load prologue.
+//   backward : drn_bn_bwd_reduce (sum g, sum g*xhat, g = dy * relu'(y)) -> drn_bn_finalize_bwd
+//              (dgamma/dbeta into the gradient buffer + per-channel coefficients)
+//              -> drn_bn_bwd_apply (dx, optionally + the identity-shortcut gradient).
+// Every kernel reads/writes 16-byte vectors (8 channels) per lane.
+#include "drn_common.h"
+
+namespace drn {
+
+// x [M][C] -> part[blockIdx][2][C]
+__global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ x, float* __restrict__ part, int M,
+                                                       int C, int rows_per_block) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int CV = C / 8;
+  const int tid = threadIdx.x;
+  const int rpp = 256 / CV;  // rows per pass (CV <= 256)
+  const int cv = tid % CV;
+  const int r0 = tid / CV;
+  float s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = q[j] = 0.f;
+  const int mbeg = blockIdx.x * rows_per_block;
+  const int mend = min(M, mbeg + rows_per_block);
+  if (r0 < rpp) {
+    for (int m = mbeg + r0; m < mend; m += rpp) {
+      const uint4 v = *reinterpret_cast<const uint4*>(x + (size_t)m * C + cv * 8);
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += f[j];
+        q[j] += f[j] * f[j];
+      }
+    }
+  }
+  float* red = reinterpret_cast<float*>(smem);  // [256][16]
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[tid * 16 + j] = s[j];
+    red[tid * 16 + 8 + j] = q[j];
+  }
+  __syncthreads();
+  // thread t < C*2 produces channel c = t>>1, which = t&1
+  for (int t = tid; t < 2 * C; t += 256) {
+    const int c = t >> 1, which = t & 1;
+    const int cvv = c / 8, j = c % 8;
+    float acc = 0.f;
+    for (int r = 0; r < rpp; ++r) acc += red[(r * CV + cvv) * 16 + which * 8 + j];
+    part[((size_t)blockIdx.x * 2 + which) * C + c] = acc;
+  }
+}
+
+// part[G][2][C] -> scale/shift (+mean, invstd), running stats update. One thread per channel.
+__global__ void bn_finalize_kernel(const float* __restrict__ part, int G, int C, float count,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                                   float momentum, float* __restrict__ run_mean, float* __restrict__ run_var,
+                                   float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ mean_out,
+                                   float* __restrict__ invstd_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int g = 0; g < G; ++g) {
+    s += part[((size_t)g * 2 + 0) * C + c];
+    q += part[((size_t)g * 2 + 1) * C + c];
+  }
+  const double mean = s / count;
+  double var = q / count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float sc = gamma[c] * invstd;
+  scale[c] = sc;
+  shift[c] = beta[c] - (float)mean * sc;
+  mean_out[c] = (float)mean;
+  invstd_out[c] = invstd;
+  if (run_mean) {
+    // moving averages (TF fused BN: unbiased batch variance feeds the moving variance)
+    const float unbiased = count > 1.f ? (float)(var * count / (count - 1.0)) : (float)var;
+    run_mean[c] = momentum * run_mean[c] + (1.f - momentum) * (float)mean;
+    run_var[c] = momentum * run_var[c] + (1.f - momentum) * unbiased;
+  }
+}
+
+__global__ void bn_inference_params_kernel(int C, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                           const float* __restrict__ run_mean, const float* __restrict__ run_var,
+                                           float eps, float* __restrict__ scale, float* __restrict__ shift,
+                                           float* __restrict__ mean_out, float* __restrict__ invstd_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float invstd = rsqrtf(run_var[c] + eps);
+  const float sc = gamma[c] * invstd;
+  scale[c] = sc;
+  shift[c] = beta[c] - run_mean[c] * sc;
+  if (mean_out) mean_out[c] = run_mean[c];
+  if (invstd_out) invstd_out[c] = invstd;
+}
+
+__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, int64_t nvec, int CV,
+                                                       int relu) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % CV) * 8;
+    float f[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[i], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f[j] = f[j] * scale[c + j] + shift[c + j];
+      if (relu) f[j] = fmaxf(f[j], 0.f);
+    }
+    reinterpret_cast<uint4*>(y)[i] = pack8(f);
+  }
+}
+
+// dy source: either a bf16 [M][C] tensor, or (pool_hw > 0) the global-average-pool gradient
+// dpool[n][c] (fp32) broadcast over the pool window: dy[m][c] = dpool[m / pool_hw][c] / pool_hw.
+struct DySrc {
+  const bf16_t* dy;
+  const float* dpool;
+  int pool_hw;
+  __device__ __forceinline__ void load(int64_t m, int C, int c, float* f) const {
+    if (pool_hw > 0) {
+      const float inv = 1.f / (float)pool_hw;
+      const float* p = dpool + (m / pool_hw) * C + c;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = p[j] * inv;
+    } else {
+      unpack8(*reinterpret_cast<const uint4*>(dy + m * C + c), f);
+    }
+  }
+};
+
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(DySrc src, const bf16_t* __restrict__ x,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ shift,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd, float* __restrict__ part,
+                                                            int M, int C, int rows_per_block, int relu) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int CV = C / 8;
+  const int tid = threadIdx.x;
+  const int rpp = 256 / CV;
+  const int cv = tid % CV;
+  const int r0 = tid / CV;
+  const int c = cv * 8;
+  float sg[8], sgx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sg[j] = sgx[j] = 0.f;
+  const int mbeg = blockIdx.x * rows_per_block;
+  const int mend = min(M, mbeg + rows_per_block);
+  if (r0 < rpp) {
+    float sc[8], sh[8], mu[8], is[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = scale[c + j]; sh[j] = shift[c + j]; mu[j] = mean[c + j]; is[j] = invstd[c + j];
+    }
+    for (int m = mbeg + r0; m < mend; m += rpp) {
+      float fx[8], fd[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + (size_t)m * C + c), fx);
+      src.load(m, C, c, fd);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float y = fx[j] * sc[j] + sh[j];
+        const float g = (relu && y <= 0.f) ? 0.f : fd[j];
+        sg[j] += g;
+        sgx[j] += g * (fx[j] - mu[j]) * is[j];
+      }
+    }
+  }
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[tid * 16 + j] = sg[j];
+    red[tid * 16 + 8 + j] = sgx[j];
+  }
+  __syncthreads();
+  for (int t = tid; t < 2 * C; t += 256) {
+    const int ch = t >> 1, which = t & 1;
+    const int cvv = ch / 8, j = ch % 8;
+    float acc = 0.f;
+    for (int r = 0; r < rpp; ++r) acc += red[(r * CV + cvv) * 16 + which * 8 + j];
+    part[((size_t)blockIdx.x * 2 + which) * C + ch] = acc;
+  }
+}
+
+// part[G][2][C] (sum g, sum g*xhat) -> dbeta, dgamma (written to the gradient buffer, scaled by
+// grad_scale and ACCUMULATED if accumulate) + apply coefficients coef[3][C]:
+//   dx = k1 * (g - k2 - xhat * k3),  k1 = gamma*invstd, k2 = sum g / M, k3 = sum g*xhat / M
+__global__ void bn_finalize_bwd_kernel(const float* __restrict__ part, int G, int C, float count,
+                                       const float* __restrict__ gamma, const float* __restrict__ invstd,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                       float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, sx = 0.0;
+  for (int g = 0; g < G; ++g) {
+    s += part[((size_t)g * 2 + 0) * C + c];
+    sx += part[((size_t)g * 2 + 1) * C + c];
+  }
+  dbeta[c] = (float)s;
+  dgamma[c] = (float)sx;
+  coef[c] = gamma[c] * invstd[c];
+  coef[C + c] = (float)(s / count);
+  coef[2 * C + c] = (float)(sx / count);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(DySrc src, const bf16_t* __restrict__ x,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ coef,
+                                                           const bf16_t* __restrict__ add, bf16_t* __restrict__ dx,
+                                                           int64_t nvec, int C, int relu) {
+  const int CV = C / 8;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / CV;
+    const int c = (int)(i - m * CV) * 8;
+    float fx[8], fd[8], fa[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[i], fx);
+    src.load(m, C, c, fd);
+    if (add) unpack8(reinterpret_cast<const uint4*>(add)[i], fa);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float y = fx[j] * scale[c + j] + shift[c + j];
+      const float g = (relu && y <= 0.f) ? 0.f : fd[j];
+      const float xh = (fx[j] - mean[c + j]) * invstd[c + j];
+      float v = coef[c + j] * (g - coef[C + c + j] - xh * coef[2 * C + c + j]);
+      if (add) v += fa[j];
+      fd[j] = v;
+    }
+    reinterpret_cast<uint4*>(dx)[i] = pack8(fd);
+  }
+}
+
+static inline int grid_for(int64_t nvec) {
+  int64_t b = (nvec + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace drn
+
+DRN_API int drn_bn_stats_blocks(int M, int C, int rows_per_block) { return (M + rows_per_block - 1) / rows_per_block; }
+
+DRN_API int drn_bn_stats(const void* x, float* part, int M, int C, int rows_per_block, hipStream_t s) {
+  if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
+  const int G = (M + rows_per_block - 1) / rows_per_block;
+  hipLaunchKernelGGL(drn::bn_stats_kernel, dim3(G), dim3(256), 256 * 16 * 4, s, (const bf16_t*)x, part, M, C,
+                     rows_per_block);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_bn_finalize(const float* part, int G, int C, float count, const float* gamma, const float* beta,
+                            float eps, float momentum, float* run_mean, float* run_var, float* scale, float* shift,
+                            float* mean, float* invstd, hipStream_t s) {
+  hipLaunchKernelGGL(drn::bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, G, C, count, gamma, beta,
+                     eps, momentum, run_mean, run_var, scale, shift, mean, invstd);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_bn_inference_params(int C, const float* gamma, const float* beta, const float* run_mean,
+                                    const float* run_var, float eps, float* scale, float* shift, float* mean,
+                                    float* invstd, hipStream_t s) {
+  hipLaunchKernelGGL(drn::bn_inference_params_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, beta,
+                     run_mean, run_var, eps, scale, shift, mean, invstd);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_bn_apply(const void* x, void* y, const float* scale, const float* shift, int64_t M, int C, int relu,
+                         hipStream_t s) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const int64_t nvec = M * (C / 8);
+  hipLaunchKernelGGL(drn::bn_apply_kernel, dim3(drn::grid_for(nvec)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y,
+                     scale, shift, nvec, C / 8, relu);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_bn_bwd_reduce(const void* dy, const float* dpool, int pool_hw, const void* x, const float* scale,
+                              const float* shift, const float* mean, const float* invstd, float* part, int M, int C,
+                              int rows_per_block, int relu, hipStream_t s) {
+  if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
+  const int G = (M + rows_per_block - 1) / rows_per_block;
+  drn::DySrc src{(const bf16_t*)dy, dpool, pool_hw};
+  hipLaunchKernelGGL(drn::bn_bwd_reduce_kernel, dim3(G), dim3(256), 256 * 16 * 4, s, src, (const bf16_t*)x, scale,
+                     shift, mean, invstd, part, M, C, rows_per_block, relu);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_bn_finalize_bwd(const float* part, int G, int C, float count, const float* gamma,
+                                const float* invstd, float* dgamma, float* dbeta, float* coef, hipStream_t s) {
+  hipLaunchKernelGGL(drn::bn_finalize_bwd_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, G, C, count, gamma,
+                     invstd, dgamma, dbeta, coef);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_bn_bwd_apply(const void* dy, const float* dpool, int pool_hw, const void* x, const float* scale,
+                             const float* shift, const float* mean, const float* invstd, const float* coef,
+                             const void* add, void* dx, int64_t M, int C, int relu, hipStream_t s) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const int64_t nvec = M * (C / 8);
+  drn::DySrc src{(const bf16_t*)dy, dpool, pool_hw};
+  hipLaunchKernelGGL(drn::bn_bwd_apply_kernel, dim3(drn::grid_for(nvec)), dim3(256), 0, s, src, (const bf16_t*)x,
+                     scale, shift, mean, invstd, coef, (const bf16_t*)add, (bf16_t*)dx, nvec, C, relu);
+  return (int)hipGetLastError();
+}

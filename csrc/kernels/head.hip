@@ -1,0 +1,186 @@
+// head.hip — classifier head on gfx950: final BN-ReLU + global average pool, dense layer
+// (fp32 GEMMs), softmax cross-entropy with one-hot labels and the batch precision metric.
+//
+// Reference: final batch_norm_relu + average_pooling2d(VALID, pool = H) + dense
+// (resnet_model_official.py:268-275 CIFAR, :336-343 ImageNet); softmax + mean
+// softmax_cross_entropy (resnet_model.py:77-80); train "precision" = mean(argmax p == argmax y)
+// (resnet_cifar_main.py:270-272).
+#include "drn_common.h"
+
+namespace drn {
+
+// pooled[n][c] = mean_hw relu(x[n][hw][c]*scale[c] + shift[c])   (scale==nullptr: no BN)
+__global__ __launch_bounds__(256) void bnrelu_pool_kernel(const bf16_t* __restrict__ x, const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, float* __restrict__ pooled,
+                                                          int HW, int C, int relu) {
+  const int n = blockIdx.x;
+  const int CV = C / 8;
+  for (int cv = threadIdx.x; cv < CV; cv += blockDim.x) {
+    const int c = cv * 8;
+    float acc[8], sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      acc[j] = 0.f;
+      sc[j] = scale ? scale[c + j] : 1.f;
+      sh[j] = scale ? shift[c + j] : 0.f;
+    }
+    for (int hw = 0; hw < HW; ++hw) {
+      float f[8];
+      unpack8(*reinterpret_cast<const uint4*>(x + ((size_t)n * HW + hw) * C + c), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = f[j] * sc[j] + sh[j];
+        if (relu) v = fmaxf(v, 0.f);
+        acc[j] += v;
+      }
+    }
+    const float inv = 1.f / (float)HW;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pooled[(size_t)n * C + c + j] = acc[j] * inv;
+  }
+}
+
+// C[M][N] = alpha * op(A) op(B) + beta * C (+ bias[N]); row-major; op = transpose if flag.
+// 64x64 tile, 256 threads (4x4 outputs each), BK = 16. fp32 (exact, off the MFMA path: the
+// head GEMMs are <1% of the step).
+__global__ __launch_bounds__(256) void sgemm_kernel(int ta, int tb, int M, int N, int K, float alpha,
+                                                    const float* __restrict__ A, int lda,
+                                                    const float* __restrict__ B, int ldb, float beta,
+                                                    float* __restrict__ Cm, int ldc, const float* __restrict__ bias) {
+  __shared__ float As[16][64 + 1];
+  __shared__ float Bs[16][64 + 1];
+  const int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  float acc[4][4] = {};
+  for (int k0 = 0; k0 < K; k0 += 16) {
+    for (int t = threadIdx.x; t < 16 * 64; t += 256) {
+      const int kk = t / 64, mm = t % 64;
+      const int gm = m0 + mm, gk = k0 + kk;
+      float va = 0.f;
+      if (gm < M && gk < K) va = ta ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk];
+      As[kk][mm] = va;
+      const int gn = n0 + mm;
+      float vb = 0.f;
+      if (gn < N && gk < K) vb = tb ? B[(size_t)gn * ldb + gk] : B[(size_t)gk * ldb + gn];
+      Bs[kk][mm] = vb;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      float a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[kk][ty * 4 + i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx * 4 + j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] += a[i] * b[j];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int gm = m0 + ty * 4 + i, gn = n0 + tx * 4 + j;
+      if (gm < M && gn < N) {
+        float v = alpha * acc[i][j];
+        if (bias) v += bias[gn];
+        if (beta != 0.f) v += beta * Cm[(size_t)gm * ldc + gn];
+        Cm[(size_t)gm * ldc + gn] = v;
+      }
+    }
+}
+
+// One block per sample: softmax, loss, dlogits = (p - y) * grad_scale, correct-count.
+// labels: int32 class ids. out_loss[n] per-sample loss; probs optional.
+__global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restrict__ logits,
+                                                           const int* __restrict__ labels, int ncls,
+                                                           float grad_scale, float* __restrict__ dlogits,
+                                                           float* __restrict__ loss, float* __restrict__ probs,
+                                                           int* __restrict__ correct) {
+  const int n = blockIdx.x;
+  const float* z = logits + (size_t)n * ncls;
+  __shared__ float sred[8];
+  __shared__ int sidx[8];
+  float mx = -INFINITY;
+  int amax = 0;
+  for (int j = threadIdx.x; j < ncls; j += blockDim.x) {
+    const float v = z[j];
+    if (v > mx) { mx = v; amax = j; }
+  }
+  // block argmax (first index of the max)
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(mx, o, 64);
+    const int oi = __shfl_xor(amax, o, 64);
+    if (ov > mx || (ov == mx && oi < amax)) { mx = ov; amax = oi; }
+  }
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, nw = blockDim.x >> 6;
+  if (l == 0) { sred[w] = mx; sidx[w] = amax; }
+  __syncthreads();
+  mx = sred[0]; amax = sidx[0];
+  for (int i = 1; i < nw; ++i)
+    if (sred[i] > mx || (sred[i] == mx && sidx[i] < amax)) { mx = sred[i]; amax = sidx[i]; }
+  __syncthreads();
+  float se = 0.f;
+  for (int j = threadIdx.x; j < ncls; j += blockDim.x) se += __expf(z[j] - mx);
+  se = wave_sum(se);
+  if (l == 0) sred[w] = se;
+  __syncthreads();
+  se = 0.f;
+  for (int i = 0; i < nw; ++i) se += sred[i];
+  const int y = labels[n];
+  const float lse = mx + __logf(se);
+  const float inv = 1.f / se;
+  for (int j = threadIdx.x; j < ncls; j += blockDim.x) {
+    const float p = __expf(z[j] - mx) * inv;
+    if (probs) probs[(size_t)n * ncls + j] = p;
+    if (dlogits) dlogits[(size_t)n * ncls + j] = (p - (j == y ? 1.f : 0.f)) * grad_scale;
+  }
+  if (threadIdx.x == 0) {
+    loss[n] = lse - z[y];
+    if (correct) correct[n] = (amax == y) ? 1 : 0;
+  }
+}
+
+// column sums: out[j] = scale * sum_n in[n][j]  (dense bias gradient)
+__global__ void colsum_kernel(const float* __restrict__ in, int rows, int cols, float* __restrict__ out, float scale,
+                              int accumulate) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= cols) return;
+  float s = 0.f;
+  for (int n = 0; n < rows; ++n) s += in[(size_t)n * cols + j];
+  out[j] = accumulate ? out[j] + scale * s : scale * s;
+}
+
+}  // namespace drn
+
+DRN_API int drn_bnrelu_pool(const void* x, const float* scale, const float* shift, float* pooled, int N, int HW,
+                            int C, int relu, hipStream_t s) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(drn::bnrelu_pool_kernel, dim3(N), dim3(256), 0, s, (const bf16_t*)x, scale, shift, pooled, HW, C,
+                     relu);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_sgemm(int ta, int tb, int M, int N, int K, float alpha, const float* A, int lda, const float* B,
+                      int ldb, float beta, float* C, int ldc, const float* bias, hipStream_t s) {
+  dim3 grid((N + 63) / 64, (M + 63) / 64);
+  hipLaunchKernelGGL(drn::sgemm_kernel, grid, dim3(256), 0, s, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc,
+                     bias);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_softmax_xent(const float* logits, const int* labels, int N, int ncls, float grad_scale,
+                             float* dlogits, float* loss, float* probs, int* correct, hipStream_t s) {
+  hipLaunchKernelGGL(drn::softmax_xent_kernel, dim3(N), dim3(256), 0, s, logits, labels, ncls, grad_scale, dlogits,
+                     loss, probs, correct);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_colsum(const float* in, int rows, int cols, float* out, float scale, int accumulate, hipStream_t s) {
+  hipLaunchKernelGGL(drn::colsum_kernel, dim3((cols + 255) / 256), dim3(256), 0, s, in, rows, cols, out, scale,
+                     accumulate);
+  return (int)hipGetLastError();
+}

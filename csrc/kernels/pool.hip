@@ -1,0 +1,112 @@
+// pool.hip — ImageNet stem max-pool 3x3/2 'SAME' (reference resnet_model_official.py:314-316)
+// forward with a per-output uint8 argmax record, and the backward as a GATHER over the
+// windows that selected each input element (no atomics, deterministic).
+// TF 'SAME' geometry: P = ceil(H/stride), pad_beg = max((P-1)*stride + k - H, 0) / 2; padded
+// taps never win (they are -inf for max pooling).
+#include "drn_common.h"
+
+namespace drn {
+
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                          uint8_t* __restrict__ arg, int N, int H, int W, int C, int P,
+                                                          int Q, int k, int stride, int pad_h, int pad_w) {
+  const int CV = C / 8;
+  const int64_t total = (int64_t)N * P * Q * CV;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % CV);
+    int64_t t = i / CV;
+    const int q = (int)(t % Q);
+    t /= Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int r = 0; r < k; ++r) {
+      const int h = p * stride - pad_h + r;
+      if (h < 0 || h >= H) continue;
+      for (int s = 0; s < k; ++s) {
+        const int w = q * stride - pad_w + s;
+        if (w < 0 || w >= W) continue;
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(x + (((size_t)n * H + h) * W + w) * C + cv * 8), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (f[j] > best[j]) { best[j] = f[j]; bi[j] = (uint8_t)(r * k + s); }
+      }
+    }
+    reinterpret_cast<uint4*>(y)[i] = pack8(best);
+    uint2 a;
+    a.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    a.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    reinterpret_cast<uint2*>(arg)[i] = a;
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                                          bf16_t* __restrict__ dx, int N, int H, int W, int C, int P,
+                                                          int Q, int k, int stride, int pad_h, int pad_w) {
+  const int CV = C / 8;
+  const int64_t total = (int64_t)N * H * W * CV;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % CV);
+    int64_t t = i / CV;
+    const int w = (int)(t % W);
+    t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    float acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    // windows p with p*stride - pad_h <= h <= p*stride - pad_h + k - 1
+    const int p_lo = max(0, (h + pad_h - k + stride) / stride);
+    const int p_hi = min(P - 1, (h + pad_h) / stride);
+    const int q_lo = max(0, (w + pad_w - k + stride) / stride);
+    const int q_hi = min(Q - 1, (w + pad_w) / stride);
+    for (int p = p_lo; p <= p_hi; ++p) {
+      const int r = h - (p * stride - pad_h);
+      if (r < 0 || r >= k) continue;
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const int s = w - (q * stride - pad_w);
+        if (s < 0 || s >= k) continue;
+        const int tap = r * k + s;
+        const size_t o = (((size_t)n * P + p) * Q + q) * CV + cv;
+        const uint2 a = reinterpret_cast<const uint2*>(arg)[o];
+        float g[8];
+        unpack8(reinterpret_cast<const uint4*>(dy)[o], g);
+        const uint8_t b[8] = {(uint8_t)(a.x), (uint8_t)(a.x >> 8), (uint8_t)(a.x >> 16), (uint8_t)(a.x >> 24),
+                              (uint8_t)(a.y), (uint8_t)(a.y >> 8), (uint8_t)(a.y >> 16), (uint8_t)(a.y >> 24)};
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (b[j] == tap) acc[j] += g[j];
+      }
+    }
+    reinterpret_cast<uint4*>(dx)[i] = pack8(acc);
+  }
+}
+
+static inline int grid_for(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
+}
+
+}  // namespace drn
+
+DRN_API int drn_maxpool_fwd(const void* x, void* y, uint8_t* arg, int N, int H, int W, int C, int P, int Q, int k,
+                            int stride, int pad_h, int pad_w, hipStream_t s) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const int64_t total = (int64_t)N * P * Q * (C / 8);
+  hipLaunchKernelGGL(drn::maxpool_fwd_kernel, dim3(drn::grid_for(total)), dim3(256), 0, s, (const bf16_t*)x,
+                     (bf16_t*)y, arg, N, H, W, C, P, Q, k, stride, pad_h, pad_w);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_maxpool_bwd(const void* dy, const uint8_t* arg, void* dx, int N, int H, int W, int C, int P, int Q,
+                            int k, int stride, int pad_h, int pad_w, hipStream_t s) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const int64_t total = (int64_t)N * H * W * (C / 8);
+  hipLaunchKernelGGL(drn::maxpool_bwd_kernel, dim3(drn::grid_for(total)), dim3(256), 0, s, (const bf16_t*)dy, arg,
+                     (bf16_t*)dx, N, H, W, C, P, Q, k, stride, pad_h, pad_w);
+  return (int)hipGetLastError();
+}

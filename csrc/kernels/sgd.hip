@@ -1,0 +1,117 @@
+// sgd.hip — fused optimizer step and weight-layout maintenance on gfx950.
+//
+// Replaces TF's per-variable ApplyMomentum + L2Loss/AddN gradient of the weight-decay term
+// (reference resnet_model.py:85-86 cost = xent + wd * sum(l2_loss(v)) over ALL trainable vars;
+// :98-99 MomentumOptimizer(lr, 0.9), non-Nesterov) with ONE launch over the flat fp32
+// master buffer (all 152/153 variables back to back):
+//   g' = g * grad_scale + wd * w ;  m = mu * m + g' ;  w -= lr * m ;  w_bf16 = bf16(w)
+// grad_scale folds the 1/world_size of the data-parallel average (SyncReplicas/Horovod mean).
+// The learning rate is read from device memory so a captured HIP graph replays with the
+// per-step LR written by the host (the reference feeds it through feed_dict each step,
+// resnet_cifar_main.py:293-296).
+#include "drn_common.h"
+
+namespace drn {
+
+__global__ __launch_bounds__(256) void sgd_momentum_kernel(float* __restrict__ w, float* __restrict__ m,
+                                                           const float* __restrict__ g, bf16_t* __restrict__ wb,
+                                                           int64_t n4, const float* __restrict__ lr_ptr, float mu,
+                                                           float wd, float grad_scale) {
+  const float lr = *lr_ptr;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 wv = reinterpret_cast<float4*>(w)[i];
+    float4 mv = reinterpret_cast<float4*>(m)[i];
+    const float4 gv = reinterpret_cast<const float4*>(g)[i];
+    float gg;
+    gg = gv.x * grad_scale + wd * wv.x; mv.x = mu * mv.x + gg; wv.x -= lr * mv.x;
+    gg = gv.y * grad_scale + wd * wv.y; mv.y = mu * mv.y + gg; wv.y -= lr * mv.y;
+    gg = gv.z * grad_scale + wd * wv.z; mv.z = mu * mv.z + gg; wv.z -= lr * mv.z;
+    gg = gv.w * grad_scale + wd * wv.w; mv.w = mu * mv.w + gg; wv.w -= lr * mv.w;
+    reinterpret_cast<float4*>(w)[i] = wv;
+    reinterpret_cast<float4*>(m)[i] = mv;
+    if (wb) {
+      uint2 o;
+      o.x = pack2bf(wv.x, wv.y);
+      o.y = pack2bf(wv.z, wv.w);
+      reinterpret_cast<uint2*>(wb)[i] = o;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y,
+                                                        int64_t n4) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    uint2 o;
+    o.x = pack2bf(v.x, v.y);
+    o.y = pack2bf(v.z, v.w);
+    reinterpret_cast<uint2*>(y)[i] = o;
+  }
+}
+
+// Data-gradient weights: Wt[c][R-1-r][S-1-s][k] = W[k][r][s][c] for a batch of convolutions
+// described by a device-resident table (one launch for the whole network).
+struct TDesc {
+  int64_t src, dst;  // element offsets into the flat bf16 weight buffers
+  int32_t K, R, S, C;
+  int64_t begin;     // prefix sum of element counts (work partition)
+};
+
+__global__ __launch_bounds__(256) void weight_tflip_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt,
+                                                           const TDesc* __restrict__ table, int ntab,
+                                                           int64_t total) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    // binary search the descriptor owning element i
+    int lo = 0, hi = ntab - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (table[mid].begin <= i) lo = mid; else hi = mid - 1;
+    }
+    const TDesc d = table[lo];
+    int64_t e = i - d.begin;  // index into destination [C][R][S][K]
+    const int k = (int)(e % d.K); e /= d.K;
+    const int s = (int)(e % d.S); e /= d.S;
+    const int r = (int)(e % d.R);
+    const int c = (int)(e / d.R);
+    const int rs = d.R - 1 - r, ssrc = d.S - 1 - s;
+    wt[d.dst + i - d.begin] = w[d.src + (((int64_t)k * d.R + rs) * d.S + ssrc) * d.C + c];
+  }
+}
+
+__global__ void fill_f32_kernel(float* __restrict__ x, int64_t n, float v) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) x[i] = v;
+}
+
+static inline int grid_for(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
+}
+
+}  // namespace drn
+
+DRN_API int drn_sgd_momentum(float* w, float* m, const float* g, void* w_bf16, int64_t n, const float* lr_ptr,
+                             float momentum, float wd, float grad_scale, hipStream_t s) {
+  if (n % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(drn::sgd_momentum_kernel, dim3(drn::grid_for(n / 4)), dim3(256), 0, s, w, m, g,
+                     (bf16_t*)w_bf16, n / 4, lr_ptr, momentum, wd, grad_scale);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_cast_bf16(const float* x, void* y, int64_t n, hipStream_t s) {
+  if (n % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(drn::cast_bf16_kernel, dim3(drn::grid_for(n / 4)), dim3(256), 0, s, x, (bf16_t*)y, n / 4);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_weight_tflip(const void* w, void* wt, const void* table, int ntab, int64_t total, hipStream_t s) {
+  hipLaunchKernelGGL(drn::weight_tflip_kernel, dim3(drn::grid_for(total)), dim3(256), 0, s, (const bf16_t*)w,
+                     (bf16_t*)wt, (const drn::TDesc*)table, ntab, total);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_fill_f32(float* x, int64_t n, float v, hipStream_t s) {
+  hipLaunchKernelGGL(drn::fill_f32_kernel, dim3(drn::grid_for(n)), dim3(256), 0, s, x, n, v);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_version() { return 1; }

@@ -1,0 +1,124 @@
+"""Loader for the in-tree gfx950 kernel library ``libdrn_kernels.so`` (ctypes, C ABI).
+
+The GPU compute path of this framework IS this library: there is no silent fallback. When a
+GPU is present and the library is missing or fails to load, :func:`lib` raises. The CPU
+reference backend (``ops.ref``) exists only for CPU-only runs (BASELINE config 1) and as the
+fp32 test oracle.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+
+import torch  # noqa: F401  (must be imported first: its HIP runtime is the one we bind to)
+
+_LIB = None
+_LOCK = threading.Lock()
+LIB_PATH = Path(__file__).resolve().parent / "libdrn_kernels.so"
+
+c_int = ctypes.c_int
+c_i64 = ctypes.c_int64
+c_f = ctypes.c_float
+c_p = ctypes.c_void_p
+
+
+class DrnFastDiv(ctypes.Structure):
+    _fields_ = [("d", ctypes.c_uint32), ("m", ctypes.c_uint32), ("s", ctypes.c_uint32), ("pad_", ctypes.c_uint32)]
+
+    @classmethod
+    def make(cls, d: int) -> "DrnFastDiv":
+        d = int(max(1, d))
+        s = 0
+        while (1 << s) < d:
+            s += 1
+        m = ((1 << 32) * ((1 << s) - d)) // d + 1
+        return cls(d, m & 0xFFFFFFFF, s, 0)
+
+
+class DrnConvFwdArgs(ctypes.Structure):
+    _fields_ = [
+        ("x", c_p), ("w", c_p), ("y", c_p), ("in_scale", c_p), ("in_shift", c_p), ("residual", c_p), ("stats", c_p),
+        ("N", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("K", c_int), ("R", c_int), ("S", c_int),
+        ("P", c_int), ("Q", c_int), ("stride", c_int), ("pad_h", c_int), ("pad_w", c_int), ("dil", c_int),
+        ("relu_in", c_int), ("tiles_p", c_int),
+    ]
+
+
+class DrnConvWgradArgs(ctypes.Structure):
+    _fields_ = [
+        ("x", c_p), ("dy", c_p), ("out", c_p), ("in_scale", c_p), ("in_shift", c_p),
+        ("N", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("K", c_int), ("R", c_int), ("S", c_int),
+        ("P", c_int), ("Q", c_int), ("stride", c_int), ("pad_h", c_int), ("pad_w", c_int), ("relu_in", c_int),
+        ("splits", c_int), ("pix_per_split", c_int), ("fd_pq", DrnFastDiv), ("fd_q", DrnFastDiv),
+    ]
+
+
+_SIGS = {
+    "drn_version": ([], c_int),
+    "drn_conv_fwd": ([ctypes.POINTER(DrnConvFwdArgs), c_p], c_int),
+    "drn_conv_fwd_tiles_p": ([c_int, c_int], c_int),
+    "drn_conv_wgrad": ([ctypes.POINTER(DrnConvWgradArgs), c_p], c_int),
+    "drn_splitk_reduce": ([c_p, c_p, c_i64, c_int, c_f, c_int, c_p], c_int),
+    "drn_bn_stats": ([c_p, c_p, c_int, c_int, c_int, c_p], c_int),
+    "drn_bn_finalize": ([c_p, c_int, c_int, c_f, c_p, c_p, c_f, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_int),
+    "drn_bn_inference_params": ([c_int, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p], c_int),
+    "drn_bn_apply": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_p], c_int),
+    "drn_bn_bwd_reduce": ([c_p, c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p], c_int),
+    "drn_bn_finalize_bwd": ([c_p, c_int, c_int, c_f, c_p, c_p, c_p, c_p, c_p, c_p], c_int),
+    "drn_bn_bwd_apply": ([c_p, c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_p], c_int),
+    "drn_bnrelu_pool": ([c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p], c_int),
+    "drn_sgemm": ([c_int, c_int, c_int, c_int, c_int, c_f, c_p, c_int, c_p, c_int, c_f, c_p, c_int, c_p, c_p], c_int),
+    "drn_softmax_xent": ([c_p, c_p, c_int, c_int, c_f, c_p, c_p, c_p, c_p, c_p], c_int),
+    "drn_colsum": ([c_p, c_int, c_int, c_p, c_f, c_int, c_p], c_int),
+    "drn_maxpool_fwd": ([c_p, c_p, c_p] + [c_int] * 10 + [c_p], c_int),
+    "drn_maxpool_bwd": ([c_p, c_p, c_p] + [c_int] * 10 + [c_p], c_int),
+    "drn_sgd_momentum": ([c_p, c_p, c_p, c_p, c_i64, c_p, c_f, c_f, c_f, c_p], c_int),
+    "drn_cast_bf16": ([c_p, c_p, c_i64, c_p], c_int),
+    "drn_weight_tflip": ([c_p, c_p, c_p, c_int, c_i64, c_p], c_int),
+    "drn_fill_f32": ([c_p, c_i64, c_f, c_p], c_int),
+    "drn_cifar_augment": ([c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p], c_int),
+    "drn_vgg_preprocess": ([c_p, c_p, c_p, c_int, c_int, c_int, c_f, c_f, c_f, c_p], c_int),
+    "drn_synthetic_images": ([c_p, c_i64, ctypes.c_uint32, c_p], c_int),
+}
+
+
+class KernelLibraryError(RuntimeError):
+    pass
+
+
+def available() -> bool:
+    return LIB_PATH.exists()
+
+
+def lib():
+    """Load (once) and return the kernel library; raise if it is missing or broken."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        if not LIB_PATH.exists():
+            if os.environ.get("DRN_AUTOBUILD", "1") == "1":
+                from . import build as _build
+                _build.build(verbose=False)
+            if not LIB_PATH.exists():
+                raise KernelLibraryError(
+                    f"{LIB_PATH} is missing: build it with `python -m distributed_resnet_tensorflow_amd.ops.build`")
+        try:
+            h = ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+        except OSError as e:  # pragma: no cover
+            raise KernelLibraryError(f"failed to load {LIB_PATH}: {e}") from e
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(h, name)
+            fn.argtypes = args
+            fn.restype = res
+        _LIB = h
+        return _LIB
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise KernelLibraryError(f"{what} failed with hipError {rc}")

@@ -1,0 +1,534 @@
+"""Compute backends behind the static-plan executor.
+
+``HipBackend`` is THE training path on MI355X: every call is one launch of a hand-written
+gfx950 kernel from ``libdrn_kernels.so`` on the current HIP stream (ctypes, raw device
+pointers — capturable into a HIP graph). ``RefBackend`` implements the identical op contract
+in fp32 PyTorch on the CPU; it is used for CPU-only runs (BASELINE config 1, the reference's
+`--num_gpus=0` CPU mode, resnet_cifar_main.py:387-390) and as the numerics oracle in tests.
+No op silently falls back from one to the other.
+
+Op contract (NHWC activations, KRSC conv weights, fp32 statistics):
+  conv_fwd(x, w, y, g, in_bn, relu_in, residual, stats)      y = conv(pre(x), w) [+ residual]
+  conv_wgrad(x, dy, out, g, in_bn, relu_in, ws, splits)      out = dW (fp32, KRSC)
+  bn_stats / bn_finalize / bn_inference / bn_apply
+  bn_bwd_reduce / bn_finalize_bwd / bn_bwd_apply
+  pool_bnrelu, sgemm, softmax_xent, colsum, maxpool_fwd/bwd, sgd_momentum, weight_tflip
+where pre(x) = relu(x * scale + shift) when in_bn = (scale, shift) is given.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+
+@dataclass(frozen=True)
+class ConvGeom:
+    """Geometry of one convolution launch (forward, or data-gradient as a forward conv)."""
+    stride: int = 1
+    pad_h: int = 0
+    pad_w: int = 0
+    dil: int = 1  # 2: zero-dilated (transposed) input, used for stride-2 data gradients
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def dgrad_geom(g: ConvGeom, R: int, S: int) -> ConvGeom:
+    """Data-gradient of a forward conv (stride s, leading pad p) as a forward conv of dY with the
+    flipped, channel-transposed weights: stride 1, leading pad k-1-p, input dilated by s."""
+    return ConvGeom(stride=1, pad_h=R - 1 - g.pad_h, pad_w=S - 1 - g.pad_w, dil=g.stride)
+
+
+def tflip_table(descs):
+    """Pack [(src, dst, K, R, S, C)] element offsets into the int64 device table of
+    drn_weight_tflip (struct TDesc: src, dst, {K,R}, {S,C}, begin)."""
+    rows, begin = [], 0
+    for src, dst, K, R, S, C in descs:
+        rows.append([src, dst, K | (R << 32), S | (C << 32), begin])
+        begin += K * R * S * C
+    return torch.tensor(rows, dtype=torch.int64).view(-1), len(rows), begin
+
+
+# ----------------------------------------------------------------------------------------------
+# HIP backend
+# ----------------------------------------------------------------------------------------------
+class HipBackend:
+    name = "hip"
+    act_dtype = torch.bfloat16
+
+    def __init__(self, device="cuda"):
+        self.device = torch.device(device)
+        self.L = _lib.lib()
+
+    def stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    # -- conv ---------------------------------------------------------------------------------
+    def conv_args(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None):
+        N, H, W, C = x.shape
+        K, R, S, C2 = w.shape
+        N2, P, Q, K2 = y.shape
+        assert C == C2 and K == K2 and N == N2, (x.shape, w.shape, y.shape)
+        assert x.is_contiguous() and w.is_contiguous() and y.is_contiguous()
+        a = _lib.DrnConvFwdArgs()
+        a.x, a.w, a.y = x.data_ptr(), w.data_ptr(), y.data_ptr()
+        a.in_scale = _ptr(in_bn[0]) if in_bn is not None else None
+        a.in_shift = _ptr(in_bn[1]) if in_bn is not None else None
+        a.residual = _ptr(residual)
+        a.stats = _ptr(stats)
+        a.N, a.H, a.W, a.C, a.K, a.R, a.S, a.P, a.Q = N, H, W, C, K, R, S, P, Q
+        a.stride, a.pad_h, a.pad_w, a.dil = g.stride, g.pad_h, g.pad_w, g.dil
+        a.relu_in = 1 if relu_in else 0
+        if stats is not None:
+            need = self.conv_stats_tiles(N * P * Q, K)
+            assert stats.numel() >= need * 2 * K, "stats buffer too small"
+        return a
+
+    def conv_stats_tiles(self, M, K):
+        return self.L.drn_conv_fwd_tiles_p(M, K)
+
+    def launch_conv(self, a):
+        _lib.check(self.L.drn_conv_fwd(ctypes.byref(a), self.stream()), "drn_conv_fwd")
+
+    def conv_fwd(self, x, w, y, g, in_bn=None, relu_in=True, residual=None, stats=None):
+        self.launch_conv(self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats))
+
+    @staticmethod
+    def wgrad_splits(M, Ktot, K):
+        """Split-K factor over output pixels so the grid has enough workgroups (>= ~2 per CU)."""
+        tiles = ((Ktot + 63) // 64) * ((K + 63) // 64 if K >= 64 else 1)
+        steps = (M + 127) // 128
+        want = max(1, min(steps, (1024 + tiles - 1) // tiles))
+        per = (steps + want - 1) // want
+        splits = (steps + per - 1) // per
+        return splits, per * 128
+
+    def wgrad_args(self, x, dy, out, g: ConvGeom, in_bn=None, relu_in=True, ws=None):
+        N, H, W, C = x.shape
+        N2, P, Q, K = dy.shape
+        Kd, R, S, Cd = out.shape
+        assert Kd == K and Cd == C and N == N2
+        M = N * P * Q
+        splits, pps = self.wgrad_splits(M, R * S * C, K)
+        a = _lib.DrnConvWgradArgs()
+        a.x, a.dy = x.data_ptr(), dy.data_ptr()
+        a.in_scale = _ptr(in_bn[0]) if in_bn is not None else None
+        a.in_shift = _ptr(in_bn[1]) if in_bn is not None else None
+        a.N, a.H, a.W, a.C, a.K, a.R, a.S, a.P, a.Q = N, H, W, C, K, R, S, P, Q
+        a.stride, a.pad_h, a.pad_w = g.stride, g.pad_h, g.pad_w
+        a.relu_in = 1 if relu_in else 0
+        a.splits, a.pix_per_split = splits, pps
+        a.fd_pq = _lib.DrnFastDiv.make(P * Q)
+        a.fd_q = _lib.DrnFastDiv.make(Q)
+        if splits == 1:
+            a.out = out.data_ptr()
+        else:
+            need = splits * out.numel()
+            assert ws is not None and ws.numel() >= need, f"wgrad workspace too small ({need})"
+            a.out = ws.data_ptr()
+        return a
+
+    def wgrad_ws_elems(self, M, K, R, S, C):
+        splits, _ = self.wgrad_splits(M, R * S * C, K)
+        return splits * K * R * S * C if splits > 1 else 0
+
+    def launch_wgrad(self, a, out):
+        st = self.stream()
+        _lib.check(self.L.drn_conv_wgrad(ctypes.byref(a), st), "drn_conv_wgrad")
+        if a.splits > 1:
+            _lib.check(self.L.drn_splitk_reduce(a.out, out.data_ptr(), out.numel(), a.splits, 1.0, 0, st),
+                       "drn_splitk_reduce")
+
+    def conv_wgrad(self, x, dy, out, g, in_bn=None, relu_in=True, ws=None):
+        self.launch_wgrad(self.wgrad_args(x, dy, out, g, in_bn, relu_in, ws), out)
+
+    # -- batch norm -----------------------------------------------------------------------------
+    @staticmethod
+    def bn_rows_per_block(M, C):
+        rpp = max(1, 256 // (C // 8))
+        G_target = 512
+        rpb = max(rpp, ((M + G_target - 1) // G_target + rpp - 1) // rpp * rpp)
+        return rpb
+
+    def bn_stats_blocks(self, M, C):
+        rpb = self.bn_rows_per_block(M, C)
+        return (M + rpb - 1) // rpb
+
+    def bn_stats(self, x, part):
+        C = x.shape[-1]
+        M = x.numel() // C
+        rpb = self.bn_rows_per_block(M, C)
+        _lib.check(self.L.drn_bn_stats(x.data_ptr(), part.data_ptr(), M, C, rpb, self.stream()), "drn_bn_stats")
+        return (M + rpb - 1) // rpb
+
+    def bn_finalize(self, part, G, count, gamma, beta, run_mean, run_var, scale, shift, mean, invstd,
+                    momentum, eps, update_running=True):
+        C = gamma.numel()
+        _lib.check(self.L.drn_bn_finalize(part.data_ptr(), G, C, float(count), gamma.data_ptr(), beta.data_ptr(),
+                                          eps, momentum, _ptr(run_mean) if update_running else None,
+                                          _ptr(run_var) if update_running else None, scale.data_ptr(),
+                                          shift.data_ptr(), mean.data_ptr(), invstd.data_ptr(), self.stream()),
+                   "drn_bn_finalize")
+
+    def bn_inference(self, gamma, beta, run_mean, run_var, eps, scale, shift, mean=None, invstd=None):
+        _lib.check(self.L.drn_bn_inference_params(gamma.numel(), gamma.data_ptr(), beta.data_ptr(),
+                                                  run_mean.data_ptr(), run_var.data_ptr(), eps, scale.data_ptr(),
+                                                  shift.data_ptr(), _ptr(mean), _ptr(invstd), self.stream()),
+                   "drn_bn_inference_params")
+
+    def bn_apply(self, x, y, scale, shift, relu=True):
+        C = x.shape[-1]
+        _lib.check(self.L.drn_bn_apply(x.data_ptr(), y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+                                       x.numel() // C, C, 1 if relu else 0, self.stream()), "drn_bn_apply")
+
+    def bn_bwd_reduce(self, dy, dpool, pool_hw, x, scale, shift, mean, invstd, part, relu=True):
+        C = x.shape[-1]
+        M = x.numel() // C
+        rpb = self.bn_rows_per_block(M, C)
+        _lib.check(self.L.drn_bn_bwd_reduce(_ptr(dy), _ptr(dpool), pool_hw, x.data_ptr(), scale.data_ptr(),
+                                            shift.data_ptr(), mean.data_ptr(), invstd.data_ptr(), part.data_ptr(),
+                                            M, C, rpb, 1 if relu else 0, self.stream()), "drn_bn_bwd_reduce")
+        return (M + rpb - 1) // rpb
+
+    def bn_finalize_bwd(self, part, G, count, gamma, invstd, dgamma, dbeta, coef):
+        _lib.check(self.L.drn_bn_finalize_bwd(part.data_ptr(), G, gamma.numel(), float(count), gamma.data_ptr(),
+                                              invstd.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(),
+                                              coef.data_ptr(), self.stream()), "drn_bn_finalize_bwd")
+
+    def bn_bwd_apply(self, dy, dpool, pool_hw, x, scale, shift, mean, invstd, coef, add, dx, relu=True):
+        C = x.shape[-1]
+        _lib.check(self.L.drn_bn_bwd_apply(_ptr(dy), _ptr(dpool), pool_hw, x.data_ptr(), scale.data_ptr(),
+                                           shift.data_ptr(), mean.data_ptr(), invstd.data_ptr(), coef.data_ptr(),
+                                           _ptr(add), dx.data_ptr(), x.numel() // C, C, 1 if relu else 0,
+                                           self.stream()), "drn_bn_bwd_apply")
+
+    # -- head -----------------------------------------------------------------------------------
+    def pool_bnrelu(self, x, scale, shift, pooled, relu=True):
+        N, H, W, C = x.shape
+        _lib.check(self.L.drn_bnrelu_pool(x.data_ptr(), _ptr(scale), _ptr(shift), pooled.data_ptr(), N, H * W, C,
+                                          1 if relu else 0, self.stream()), "drn_bnrelu_pool")
+
+    def sgemm(self, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias=None):
+        _lib.check(self.L.drn_sgemm(int(ta), int(tb), M, N, K, float(alpha), A.data_ptr(), lda, B.data_ptr(), ldb,
+                                    float(beta), C.data_ptr(), ldc, _ptr(bias), self.stream()), "drn_sgemm")
+
+    def softmax_xent(self, logits, labels, grad_scale, dlogits, loss, correct, probs=None):
+        N, ncls = logits.shape
+        _lib.check(self.L.drn_softmax_xent(logits.data_ptr(), labels.data_ptr(), N, ncls, float(grad_scale),
+                                           _ptr(dlogits), loss.data_ptr(), _ptr(probs), _ptr(correct),
+                                           self.stream()), "drn_softmax_xent")
+
+    def colsum(self, x, out, scale=1.0, accumulate=False):
+        rows, cols = x.shape
+        _lib.check(self.L.drn_colsum(x.data_ptr(), rows, cols, out.data_ptr(), float(scale), int(accumulate),
+                                     self.stream()), "drn_colsum")
+
+    # -- pooling --------------------------------------------------------------------------------
+    def maxpool_fwd(self, x, y, arg, k, stride, pad_h, pad_w):
+        N, H, W, C = x.shape
+        _, P, Q, _ = y.shape
+        _lib.check(self.L.drn_maxpool_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), N, H, W, C, P, Q, k, stride,
+                                          pad_h, pad_w, self.stream()), "drn_maxpool_fwd")
+
+    def maxpool_bwd(self, dy, arg, dx, k, stride, pad_h, pad_w):
+        N, H, W, C = dx.shape
+        _, P, Q, _ = dy.shape
+        _lib.check(self.L.drn_maxpool_bwd(dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), N, H, W, C, P, Q, k, stride,
+                                          pad_h, pad_w, self.stream()), "drn_maxpool_bwd")
+
+    # -- optimizer / weights ------------------------------------------------------------------------
+    def sgd_momentum(self, w, m, g, wb, lr_t, momentum, wd, grad_scale):
+        _lib.check(self.L.drn_sgd_momentum(w.data_ptr(), m.data_ptr(), g.data_ptr(), _ptr(wb), w.numel(),
+                                           lr_t.data_ptr(), float(momentum), float(wd), float(grad_scale),
+                                           self.stream()), "drn_sgd_momentum")
+
+    def cast_bf16(self, x, y):
+        _lib.check(self.L.drn_cast_bf16(x.data_ptr(), y.data_ptr(), x.numel(), self.stream()), "drn_cast_bf16")
+
+    def weight_tflip(self, wb, wt, table, ntab, total):
+        _lib.check(self.L.drn_weight_tflip(wb.data_ptr(), wt.data_ptr(), table.data_ptr(), ntab, total,
+                                           self.stream()), "drn_weight_tflip")
+
+    def zero_(self, t):
+        t.zero_()
+
+    # -- input ----------------------------------------------------------------------------------
+    def cifar_augment(self, raw_u8, params_i32, out, pad):
+        N, H, W, _ = raw_u8.shape
+        _lib.check(self.L.drn_cifar_augment(raw_u8.data_ptr(), params_i32.data_ptr(), out.data_ptr(), N, H, W, pad,
+                                            self.stream()), "drn_cifar_augment")
+
+    def vgg_preprocess(self, packed_u8, desc_i32, out, means):
+        N, OH, OW, _ = out.shape
+        _lib.check(self.L.drn_vgg_preprocess(packed_u8.data_ptr(), desc_i32.data_ptr(), out.data_ptr(), N, OH, OW,
+                                             float(means[0]), float(means[1]), float(means[2]), self.stream()),
+                   "drn_vgg_preprocess")
+
+    def synthetic_images(self, out, seed):
+        N, H, W, C = out.shape
+        assert C == 8
+        _lib.check(self.L.drn_synthetic_images(out.data_ptr(), N * H * W, seed & 0xFFFFFFFF, self.stream()),
+                   "drn_synthetic_images")
+
+
+# ----------------------------------------------------------------------------------------------
+# fp32 reference backend (CPU runs + test oracle)
+# ----------------------------------------------------------------------------------------------
+def _pre(x, in_bn, relu_in):
+    if in_bn is None:
+        return x.float()
+    y = x.float() * in_bn[0].float() + in_bn[1].float()
+    return torch.relu(y) if relu_in else y
+
+
+def _pad_for(xc, P, Q, R, S, g: ConvGeom):
+    """Pad/crop an NCHW (virtual) input so a VALID conv with stride g.stride yields P x Q."""
+    Hv, Wv = xc.shape[2], xc.shape[3]
+    pb = (P - 1) * g.stride + R - g.pad_h - Hv
+    pr = (Q - 1) * g.stride + S - g.pad_w - Wv
+    return F.pad(xc, (g.pad_w, pr, g.pad_h, pb))
+
+
+def _dilate(xc, dil):
+    if dil == 1:
+        return xc
+    N, C, H, W = xc.shape
+    out = xc.new_zeros(N, C, (H - 1) * dil + 1, (W - 1) * dil + 1)
+    out[:, :, ::dil, ::dil] = xc
+    return out
+
+
+class RefBackend:
+    name = "ref"
+    act_dtype = torch.float32
+
+    def __init__(self, device="cpu"):
+        self.device = torch.device(device)
+
+    def stream(self):
+        return None
+
+    def conv_fwd(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None):
+        K, R, S, C = w.shape
+        _, P, Q, _ = y.shape
+        xc = _dilate(_pre(x, in_bn, relu_in).permute(0, 3, 1, 2), g.dil)
+        xc = _pad_for(xc, P, Q, R, S, g)
+        out = F.conv2d(xc, w.float().permute(0, 3, 1, 2), stride=g.stride).permute(0, 2, 3, 1)
+        if residual is not None:
+            out = out + residual.float()
+        y.copy_(out)
+        if stats is not None:
+            yy = y.float().reshape(-1, K)
+            stats.zero_()
+            stats.view(-1)[:K].copy_(yy.sum(0))
+            stats.view(-1)[K:2 * K].copy_((yy * yy).sum(0))
+
+    def conv_stats_tiles(self, M, K):
+        return 1
+
+    def wgrad_ws_elems(self, M, K, R, S, C):
+        return 0
+
+    def conv_wgrad(self, x, dy, out, g: ConvGeom, in_bn=None, relu_in=True, ws=None):
+        K, R, S, C = out.shape
+        _, P, Q, _ = dy.shape
+        xc = _pad_for(_pre(x, in_bn, relu_in).permute(0, 3, 1, 2), P, Q, R, S, g)
+        dw = torch.nn.grad.conv2d_weight(xc, (K, C, R, S), dy.float().permute(0, 3, 1, 2), stride=g.stride)
+        out.copy_(dw.permute(0, 2, 3, 1))
+
+    def bn_stats_blocks(self, M, C):
+        return 1
+
+    def bn_stats(self, x, part):
+        C = x.shape[-1]
+        xx = x.float().reshape(-1, C)
+        part.view(-1)[:C].copy_(xx.sum(0))
+        part.view(-1)[C:2 * C].copy_((xx * xx).sum(0))
+        return 1
+
+    def bn_finalize(self, part, G, count, gamma, beta, run_mean, run_var, scale, shift, mean, invstd,
+                    momentum, eps, update_running=True):
+        C = gamma.numel()
+        p = part.view(-1)[:G * 2 * C].view(G, 2, C).double().sum(0)
+        mu = p[0] / count
+        var = (p[1] / count - mu * mu).clamp_min(0)
+        istd = 1.0 / torch.sqrt(var + eps)
+        scale.copy_(gamma * istd.float())
+        shift.copy_(beta - mu.float() * scale)
+        mean.copy_(mu.float())
+        invstd.copy_(istd.float())
+        if update_running:
+            unb = var * count / (count - 1) if count > 1 else var
+            run_mean.mul_(momentum).add_((1 - momentum) * mu.float())
+            run_var.mul_(momentum).add_((1 - momentum) * unb.float())
+
+    def bn_inference(self, gamma, beta, run_mean, run_var, eps, scale, shift, mean=None, invstd=None):
+        istd = torch.rsqrt(run_var + eps)
+        scale.copy_(gamma * istd)
+        shift.copy_(beta - run_mean * scale)
+        if mean is not None:
+            mean.copy_(run_mean)
+        if invstd is not None:
+            invstd.copy_(istd)
+
+    def bn_apply(self, x, y, scale, shift, relu=True):
+        v = x.float() * scale + shift
+        y.copy_(torch.relu(v) if relu else v)
+
+    def _dy(self, dy, dpool, pool_hw, x):
+        if pool_hw > 0:
+            N, H, W, C = x.shape
+            return (dpool.view(N, 1, 1, C) / pool_hw).expand(N, H, W, C)
+        return dy.float()
+
+    def bn_bwd_reduce(self, dy, dpool, pool_hw, x, scale, shift, mean, invstd, part, relu=True):
+        C = x.shape[-1]
+        d = self._dy(dy, dpool, pool_hw, x).reshape(-1, C)
+        xx = x.float().reshape(-1, C)
+        if relu:
+            d = d * ((xx * scale + shift) > 0).float()
+        xh = (xx - mean) * invstd
+        part.view(-1)[:C].copy_(d.sum(0))
+        part.view(-1)[C:2 * C].copy_((d * xh).sum(0))
+        return 1
+
+    def bn_finalize_bwd(self, part, G, count, gamma, invstd, dgamma, dbeta, coef):
+        C = gamma.numel()
+        p = part.view(-1)[:G * 2 * C].view(G, 2, C).double().sum(0)
+        dbeta.copy_(p[0].float())
+        dgamma.copy_(p[1].float())
+        coef.view(3, C)[0].copy_(gamma * invstd)
+        coef.view(3, C)[1].copy_((p[0] / count).float())
+        coef.view(3, C)[2].copy_((p[1] / count).float())
+
+    def bn_bwd_apply(self, dy, dpool, pool_hw, x, scale, shift, mean, invstd, coef, add, dx, relu=True):
+        C = x.shape[-1]
+        shp = x.shape
+        d = self._dy(dy, dpool, pool_hw, x).reshape(-1, C)
+        xx = x.float().reshape(-1, C)
+        if relu:
+            d = d * ((xx * scale + shift) > 0).float()
+        xh = (xx - mean) * invstd
+        k = coef.view(3, C)
+        v = k[0] * (d - k[1] - xh * k[2])
+        if add is not None:
+            v = v + add.float().reshape(-1, C)
+        dx.copy_(v.reshape(shp))
+
+    def pool_bnrelu(self, x, scale, shift, pooled, relu=True):
+        v = x.float()
+        if scale is not None:
+            v = v * scale + shift
+        if relu:
+            v = torch.relu(v)
+        pooled.copy_(v.mean(dim=(1, 2)))
+
+    def sgemm(self, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias=None):
+        a = A.view(-1)[: (K if ta else M) * lda].view(K if ta else M, lda)
+        a = a[:, :M].t() if ta else a[:, :K]
+        b = B.view(-1)[: (N if tb else K) * ldb].view(N if tb else K, ldb)
+        b = b[:, :K].t() if tb else b[:, :N]
+        out = alpha * (a @ b)
+        if bias is not None:
+            out = out + bias
+        cv = C.view(-1)[: M * ldc].view(M, ldc)[:, :N]
+        if beta != 0:
+            out = out + beta * cv
+        cv.copy_(out)
+
+    def softmax_xent(self, logits, labels, grad_scale, dlogits, loss, correct, probs=None):
+        lp = torch.log_softmax(logits.float(), dim=1)
+        p = lp.exp()
+        lab = labels.long()
+        loss.copy_(-lp.gather(1, lab[:, None])[:, 0])
+        if probs is not None:
+            probs.copy_(p)
+        if dlogits is not None:
+            oh = F.one_hot(lab, logits.shape[1]).float()
+            dlogits.copy_((p - oh) * grad_scale)
+        if correct is not None:
+            correct.copy_((logits.argmax(1) == lab).int())
+
+    def colsum(self, x, out, scale=1.0, accumulate=False):
+        s = x.sum(0) * scale
+        if accumulate:
+            out.add_(s)
+        else:
+            out.copy_(s)
+
+    def maxpool_fwd(self, x, y, arg, k, stride, pad_h, pad_w):
+        N, H, W, C = x.shape
+        _, P, Q, _ = y.shape
+        xc = x.float().permute(0, 3, 1, 2)
+        pb = (P - 1) * stride + k - pad_h - H
+        pr = (Q - 1) * stride + k - pad_w - W
+        xp = F.pad(xc, (pad_w, pr, pad_h, pb), value=float("-inf"))
+        win = xp.unfold(2, k, stride).unfold(3, k, stride)  # N C P Q k k
+        flat = win.reshape(N, C, P, Q, k * k)
+        v, i = flat.max(-1)
+        y.copy_(v.permute(0, 2, 3, 1))
+        arg.copy_(i.permute(0, 2, 3, 1).to(torch.uint8))
+
+    def maxpool_bwd(self, dy, arg, dx, k, stride, pad_h, pad_w):
+        N, H, W, C = dx.shape
+        _, P, Q, _ = dy.shape
+        Hp = (P - 1) * stride + k
+        Wp = (Q - 1) * stride + k
+        acc = torch.zeros(N, max(Hp, H + pad_h), max(Wp, W + pad_w), C, dtype=torch.float32)
+        a = arg.long()
+        d = dy.float()
+        for r in range(k):
+            for s in range(k):
+                m = (a == r * k + s).float() * d
+                acc[:, r:r + (P - 1) * stride + 1:stride, s:s + (Q - 1) * stride + 1:stride, :] += m
+        dx.copy_(acc[:, pad_h:pad_h + H, pad_w:pad_w + W, :])
+
+    def sgd_momentum(self, w, m, g, wb, lr_t, momentum, wd, grad_scale):
+        lr = float(lr_t.reshape(-1)[0])
+        gg = g * grad_scale + wd * w
+        m.mul_(momentum).add_(gg)
+        w.sub_(lr * m)
+        if wb is not None and wb.data_ptr() != w.data_ptr():
+            wb.copy_(w)
+
+    def cast_bf16(self, x, y):
+        y.copy_(x)
+
+    def weight_tflip(self, wb, wt, table, ntab, total):
+        for d in table.view(-1, 5).tolist()[:ntab]:
+            src, dst, kr, sc, _begin = d
+            K, R = kr & 0xFFFFFFFF, kr >> 32
+            S, C = sc & 0xFFFFFFFF, sc >> 32
+            n = K * R * S * C
+            w = wb.view(-1)[src:src + n].view(K, R, S, C)
+            wt.view(-1)[dst:dst + n].view(C, R, S, K).copy_(w.flip(1, 2).permute(3, 1, 2, 0))
+
+    def zero_(self, t):
+        t.zero_()
+
+    def cifar_augment(self, raw_u8, params_i32, out, pad):
+        N, H, W, _ = raw_u8.shape
+        img = raw_u8.float()
+        res = torch.zeros(N, H, W, out.shape[-1])
+        for n in range(N):
+            oy, ox, flip = [int(v) for v in params_i32[n].tolist()]
+            padded = F.pad(img[n].permute(2, 0, 1), (pad, pad, pad, pad))
+            crop = padded[:, oy:oy + H, ox:ox + W]
+            if flip:
+                crop = crop.flip(2)
+            mean = crop.mean()
+            std = crop.std(unbiased=False)
+            adj = torch.maximum(std, torch.tensor(1.0 / (crop.numel() ** 0.5)))
+            res[n, :, :, :3] = ((crop - mean) / adj).permute(1, 2, 0)
+        out.copy_(res)
+
+    def synthetic_images(self, out, seed):
+        g = torch.Generator().manual_seed(int(seed))
+        out.zero_()
+        out[..., :3] = torch.rand(out.shape[:-1] + (3,), generator=g) * 2 - 1

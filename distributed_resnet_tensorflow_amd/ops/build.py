@@ -1,0 +1,89 @@
+"""In-tree builder for the gfx950 HIP kernel library (``libdrn_kernels.so``).
+
+Every ``csrc/kernels/*.hip`` translation unit is compiled by ``hipcc --offload-arch=gfx950``
+into an object (in parallel, incrementally) and linked into one shared library next to this
+file. The library exposes a plain C ABI (``DRN_API`` functions in csrc/) that the runtime
+calls through ctypes with raw device pointers and the current HIP stream, so it does not link
+against libtorch and compiles in seconds. At load time the HIP runtime symbol
+``libamdhip64.so.7`` resolves to the copy PyTorch already loaded (same SONAME), so kernels and
+torch share one runtime, one device context and one set of streams.
+
+The reference has no native code at all; this replaces the cuDNN / MKL-DNN
+kernels its TF1 graph dispatched to.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[2]
+CSRC = REPO / "csrc"
+KERNELS = CSRC / "kernels"
+INCLUDE = CSRC / "include"
+LIB_DIR = Path(__file__).resolve().parent
+LIB_PATH = LIB_DIR / "libdrn_kernels.so"
+OBJ_DIR = REPO / "build" / "obj"
+ARCH = os.environ.get("DRN_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the gfx950 kernel library cannot be built")
+
+
+def sources() -> list[Path]:
+    return sorted(KERNELS.glob("*.hip"))
+
+
+def _headers_mtime() -> float:
+    hs = list(INCLUDE.glob("*.h"))
+    return max((h.stat().st_mtime for h in hs), default=0.0)
+
+
+def _compile(src: Path, extra: list[str]) -> Path:
+    obj = OBJ_DIR / (src.stem + ".o")
+    if obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, _headers_mtime()):
+        return obj
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-I", str(INCLUDE),
+           "-Wno-unused-result", "-c", str(src), "-o", str(obj)] + extra
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{res.stderr[-6000:]}")
+    return obj
+
+
+def build(force: bool = False, verbose: bool = True, extra: list[str] | None = None) -> Path:
+    """Compile all kernels for gfx950 and link libdrn_kernels.so (incremental)."""
+    OBJ_DIR.mkdir(parents=True, exist_ok=True)
+    srcs = sources()
+    if force:
+        for o in OBJ_DIR.glob("*.o"):
+            o.unlink()
+    extra = list(extra or [])
+    jobs = min(len(srcs), max(1, min(8, (os.cpu_count() or 4))))
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, extra), srcs))
+    newest = max(o.stat().st_mtime for o in objs)
+    if LIB_PATH.exists() and LIB_PATH.stat().st_mtime >= newest and not force:
+        if verbose:
+            print(f"[drn.build] up to date: {LIB_PATH}")
+        return LIB_PATH
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + [str(o) for o in objs]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"link failed:\n{res.stderr[-6000:]}")
+    os.replace(tmp, LIB_PATH)
+    if verbose:
+        print(f"[drn.build] built {LIB_PATH} from {len(objs)} translation units for {ARCH}")
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

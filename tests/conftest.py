@@ -1,0 +1,28 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and the in-tree HIP kernel library")
+    config.addinivalue_line("markers", "slow: long-running integration test")
+
+
+@pytest.fixture(scope="session")
+def hip():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU visible")
+    from distributed_resnet_tensorflow_amd.ops.backend import HipBackend
+    return HipBackend("cuda")
+
+
+@pytest.fixture(scope="session")
+def ref():
+    from distributed_resnet_tensorflow_amd.ops.backend import RefBackend
+    return RefBackend("cpu")

@@ -1,0 +1,24 @@
+// Probe of gfx950 ds_read_b64_tr_b16 semantics: LDS[r][c] = r*64+c (16-bit), 64-col rows.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+__global__ void probe(short* out) {
+  __shared__ short lds[64 * 64];
+  for (int i = threadIdx.x; i < 64 * 64; i += 64) lds[i] = (short)i;
+  __syncthreads();
+  const int l = threadIdx.x, g = l >> 4, q = (l >> 2) & 3, p = l & 3;
+  const int row = 4 * g + q, col = 4 * p;   // lane 4q+p of group g -> row 4g+q, cols 4p..4p+3
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(lds + row * 64 + col));
+  for (int e = 0; e < 4; ++e) out[l * 4 + e] = v[e];
+}
+int main() {
+  short* d; hipMalloc(&d, 64 * 4 * 2);
+  probe<<<1, 64>>>(d);
+  short h[256]; hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+  for (int l = 0; l < 64; ++l) {
+    printf("lane %2d:", l);
+    for (int e = 0; e < 4; ++e) printf(" (r%d,c%d)", h[l * 4 + e] / 64, h[l * 4 + e] % 64);
+    printf("\n");
+  }
+  return 0;
+}

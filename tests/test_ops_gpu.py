@@ -1,0 +1,280 @@
+"""Numerics of every hand-written gfx950 kernel vs the fp32 PyTorch reference of the same op.
+
+Inputs are rounded to bf16 once and fed to both sides; the reference then runs in fp32, so
+the difference is accumulation order + the bf16 rounding of the kernel output.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from distributed_resnet_tensorflow_amd.ops.backend import ConvGeom, dgrad_geom, tflip_table
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a = a.float().cpu()
+    b = b.float().cpu()
+    return (a - b).norm().item() / max(b.norm().item(), 1e-12)
+
+
+def bf(t):
+    return t.to(torch.bfloat16)
+
+
+CONV_CASES = [
+    # N, H, W, C, K, R, stride, pad
+    (2, 8, 8, 16, 16, 3, 1, 1),
+    (2, 8, 8, 16, 32, 3, 1, 1),
+    (3, 9, 9, 32, 64, 3, 2, 1),
+    (2, 7, 7, 64, 256, 1, 1, 0),
+    (2, 14, 14, 128, 128, 3, 2, 1),
+    (2, 16, 16, 8, 64, 7, 2, 3),
+    (2, 6, 6, 64, 64, 1, 2, 0),
+    (1, 5, 5, 256, 512, 3, 1, 1),
+]
+
+
+def out_size(H, R, stride, pad):
+    if stride == 1:
+        return H
+    return (H + (R - 1) - R) // stride + 1
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("fused", [False, True])
+def test_conv_fwd(hip, ref, case, fused):
+    N, H, W, C, K, R, s, p = case
+    torch.manual_seed(0)
+    P = out_size(H, R, s, p)
+    x = bf(torch.randn(N, H, W, C))
+    w = bf(torch.randn(K, R, R, C) * (2.0 / (R * R * C)) ** 0.5)
+    g = ConvGeom(stride=s, pad_h=p, pad_w=p)
+    in_bn = None
+    res = None
+    if fused:
+        in_bn = (torch.rand(C) + 0.5, torch.randn(C) * 0.1)
+        res = bf(torch.randn(N, P, P, K))
+    y_ref = torch.zeros(N, P, P, K)
+    st_ref = torch.zeros(2 * K)
+    ref.conv_fwd(x.float(), w.float(), y_ref, g, in_bn=in_bn, residual=None if res is None else res.float(),
+                 stats=st_ref)
+    y = torch.zeros(N, P, P, K, dtype=torch.bfloat16, device="cuda")
+    tiles = hip.conv_stats_tiles(N * P * P, K)
+    st = torch.zeros(tiles, 2, K, device="cuda")
+    hip.conv_fwd(x.cuda(), w.cuda(), y, g,
+                 in_bn=None if in_bn is None else (in_bn[0].cuda(), in_bn[1].cuda()),
+                 residual=None if res is None else res.cuda(), stats=st)
+    torch.cuda.synchronize()
+    assert rel(y, y_ref) < 1e-2
+    s_hip = st.sum(0).view(-1).cpu()
+    assert rel(s_hip[:K], st_ref[:K]) < 2e-2
+    assert rel(s_hip[K:], st_ref[K:]) < 2e-2
+
+
+@pytest.mark.parametrize("case", CONV_CASES[:-1])
+def test_conv_dgrad_matches_autograd(hip, case):
+    N, H, W, C, K, R, s, p = case
+    if C == 8:
+        pytest.skip("stem has no data gradient")
+    torch.manual_seed(1)
+    P = out_size(H, R, s, p)
+    x = bf(torch.randn(N, H, W, C)).float().requires_grad_(True)
+    w = bf(torch.randn(K, R, R, C) * 0.1).float()
+    g = ConvGeom(stride=s, pad_h=p, pad_w=p)
+    dy = bf(torch.randn(N, P, P, K))
+    # autograd oracle through the reference's fixed padding semantics
+    xc = x.permute(0, 3, 1, 2)
+    pb = (P - 1) * s + R - p - H
+    y = F.conv2d(F.pad(xc, (p, pb, p, pb)), w.permute(0, 3, 1, 2), stride=s)
+    y.backward(dy.float().permute(0, 3, 1, 2))
+    dx_ref = x.grad
+    wt = w.flip(1, 2).permute(3, 1, 2, 0).contiguous()  # [C][R][S][K]
+    dx = torch.zeros(N, H, W, C, dtype=torch.bfloat16, device="cuda")
+    hip.conv_fwd(dy.cuda(), bf(wt).cuda(), dx, dgrad_geom(g, R, R))
+    torch.cuda.synchronize()
+    assert rel(dx, dx_ref) < 1e-2
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("fused", [False, True])
+def test_conv_wgrad(hip, ref, case, fused):
+    N, H, W, C, K, R, s, p = case
+    torch.manual_seed(2)
+    P = out_size(H, R, s, p)
+    x = bf(torch.randn(N, H, W, C))
+    dy = bf(torch.randn(N, P, P, K))
+    g = ConvGeom(stride=s, pad_h=p, pad_w=p)
+    in_bn = (torch.rand(C) + 0.5, torch.randn(C) * 0.1) if fused else None
+    dw_ref = torch.zeros(K, R, R, C)
+    ref.conv_wgrad(x.float(), dy.float(), dw_ref, g, in_bn=in_bn)
+    dw = torch.zeros(K, R, R, C, device="cuda")
+    ws = torch.zeros(max(1, hip.wgrad_ws_elems(N * P * P, K, R, R, C)), device="cuda")
+    hip.conv_wgrad(x.cuda(), dy.cuda(), dw, g, in_bn=None if in_bn is None else (in_bn[0].cuda(), in_bn[1].cuda()),
+                   ws=ws)
+    torch.cuda.synchronize()
+    assert rel(dw, dw_ref) < 1e-2
+
+
+def test_conv_wgrad_large_splitk(hip, ref):
+    N, H, C, K = 16, 28, 64, 64
+    torch.manual_seed(3)
+    x = bf(torch.randn(N, H, H, C))
+    dy = bf(torch.randn(N, H, H, K))
+    g = ConvGeom(1, 1, 1)
+    dw_ref = torch.zeros(K, 3, 3, C)
+    ref.conv_wgrad(x.float(), dy.float(), dw_ref, g)
+    dw = torch.zeros(K, 3, 3, C, device="cuda")
+    ws = torch.zeros(max(1, hip.wgrad_ws_elems(N * H * H, K, 3, 3, C)), device="cuda")
+    hip.conv_wgrad(x.cuda(), dy.cuda(), dw, g, ws=ws)
+    torch.cuda.synchronize()
+    assert rel(dw, dw_ref) < 1e-2
+
+
+@pytest.mark.parametrize("C", [16, 64, 256, 2048])
+def test_bn_forward_and_backward(hip, ref, C):
+    torch.manual_seed(4)
+    N, H = 4, 5
+    x = bf(torch.randn(N, H, H, C) * 2 + 0.5)
+    gamma, beta = torch.rand(C) + 0.5, torch.randn(C) * 0.2
+    dy0 = bf(torch.randn(N, H, H, C))
+    add0 = bf(torch.randn(N, H, H, C))
+    outs = {}
+    for be, dev in ((ref, "cpu"), (hip, "cuda")):
+        xx = x.to(dev) if dev == "cuda" else x.float()
+        G = be.bn_stats_blocks(N * H * H, C)
+        part = torch.zeros(G, 2, C, device=dev)
+        G = be.bn_stats(xx, part)
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        sc, sh, mu, isd = (torch.zeros(C, device=dev) for _ in range(4))
+        be.bn_finalize(part, G, N * H * H, gamma.to(dev), beta.to(dev), rm, rv, sc, sh, mu, isd, 0.997, 1e-5)
+        y = torch.zeros_like(xx)
+        be.bn_apply(xx, y, sc, sh, relu=True)
+        dy = dy0.to(dev) if dev == "cuda" else dy0.float()
+        add = add0.to(dev) if dev == "cuda" else add0.float()
+        Gb = be.bn_stats_blocks(N * H * H, C)
+        partb = torch.zeros(Gb, 2, C, device=dev)
+        Gb = be.bn_bwd_reduce(dy, None, 0, xx, sc, sh, mu, isd, partb)
+        dg, db, coef = torch.zeros(C, device=dev), torch.zeros(C, device=dev), torch.zeros(3 * C, device=dev)
+        be.bn_finalize_bwd(partb, Gb, N * H * H, gamma.to(dev), isd, dg, db, coef)
+        dx = torch.zeros_like(xx)
+        be.bn_bwd_apply(dy, None, 0, xx, sc, sh, mu, isd, coef, add, dx)
+        outs[be.name] = [t.float().cpu() for t in (sc, sh, rm, rv, y, dg, db, dx)]
+    for a, b in zip(outs["hip"], outs["ref"]):
+        assert rel(a, b) < 1e-2
+
+
+def test_bn_autograd_oracle(ref):
+    """The hand-written BN-ReLU backward equals autograd of batch-norm + relu (CPU oracle)."""
+    torch.manual_seed(5)
+    N, H, C = 3, 4, 16
+    x = torch.randn(N, H, H, C, requires_grad=True)
+    gamma = (torch.rand(C) + 0.5).requires_grad_(True)
+    beta = (torch.randn(C) * 0.1).requires_grad_(True)
+    y = torch.relu(F.batch_norm(x.permute(0, 3, 1, 2), None, None, gamma, beta, training=True, eps=1e-5))
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xd = x.detach()
+    part = torch.zeros(1, 2, C)
+    ref.bn_stats(xd, part)
+    sc, sh, mu, isd = (torch.zeros(C) for _ in range(4))
+    ref.bn_finalize(part, 1, N * H * H, gamma.detach(), beta.detach(), None, None, sc, sh, mu, isd, 0.997, 1e-5,
+                    update_running=False)
+    dyn = dy.permute(0, 2, 3, 1).contiguous()
+    partb = torch.zeros(1, 2, C)
+    ref.bn_bwd_reduce(dyn, None, 0, xd, sc, sh, mu, isd, partb)
+    dg, db, coef = torch.zeros(C), torch.zeros(C), torch.zeros(3 * C)
+    ref.bn_finalize_bwd(partb, 1, N * H * H, gamma.detach(), isd, dg, db, coef)
+    dx = torch.zeros_like(xd)
+    ref.bn_bwd_apply(dyn, None, 0, xd, sc, sh, mu, isd, coef, None, dx)
+    assert torch.allclose(dx, x.grad, atol=1e-4, rtol=1e-3)
+    assert torch.allclose(dg, gamma.grad, atol=1e-4, rtol=1e-3)
+    assert torch.allclose(db, beta.grad, atol=1e-4, rtol=1e-3)
+
+
+def test_head(hip, ref):
+    torch.manual_seed(6)
+    N, H, C, ncls = 8, 7, 2048, 1001
+    x = bf(torch.randn(N, H, H, C))
+    sc, sh = torch.rand(C) + 0.5, torch.randn(C) * 0.1
+    Wd = torch.randn(ncls, C) * 0.02
+    b = torch.randn(ncls) * 0.1
+    labels = torch.randint(0, ncls, (N,), dtype=torch.int32)
+    res = {}
+    for be, dev in ((ref, "cpu"), (hip, "cuda")):
+        xx = x.cuda() if dev == "cuda" else x.float()
+        pooled = torch.zeros(N, C, device=dev)
+        be.pool_bnrelu(xx, sc.to(dev), sh.to(dev), pooled)
+        logits = torch.zeros(N, ncls, device=dev)
+        be.sgemm(0, 1, N, ncls, C, 1.0, pooled, C, Wd.to(dev), C, 0.0, logits, ncls, bias=b.to(dev))
+        dl = torch.zeros(N, ncls, device=dev)
+        loss = torch.zeros(N, device=dev)
+        corr = torch.zeros(N, dtype=torch.int32, device=dev)
+        be.softmax_xent(logits, labels.to(dev), 1.0 / N, dl, loss, corr)
+        dW = torch.zeros(ncls, C, device=dev)
+        be.sgemm(1, 0, ncls, C, N, 1.0, dl, ncls, pooled, C, 0.0, dW, C)
+        dpool = torch.zeros(N, C, device=dev)
+        be.sgemm(0, 0, N, C, ncls, 1.0, dl, ncls, Wd.to(dev), C, 0.0, dpool, C)
+        dbias = torch.zeros(ncls, device=dev)
+        be.colsum(dl, dbias)
+        res[be.name] = [t.float().cpu() for t in (pooled, logits, dl, loss, corr, dW, dpool, dbias)]
+    for a, b2 in zip(res["hip"], res["ref"]):
+        assert rel(a, b2) < 2e-3
+
+
+def test_maxpool(hip, ref):
+    torch.manual_seed(7)
+    N, H, C = 2, 12, 64
+    P = 6
+    x = bf(torch.randn(N, H, H, C))
+    dy = bf(torch.randn(N, P, P, C))
+    out = {}
+    for be, dev in ((ref, "cpu"), (hip, "cuda")):
+        xx = x.cuda() if dev == "cuda" else x.float()
+        y = torch.zeros(N, P, P, C, dtype=xx.dtype, device=dev)
+        arg = torch.zeros(N, P, P, C, dtype=torch.uint8, device=dev)
+        be.maxpool_fwd(xx, y, arg, 3, 2, 0, 0)
+        dx = torch.zeros_like(xx)
+        be.maxpool_bwd(dy.to(dev) if dev == "cuda" else dy.float(), arg, dx, 3, 2, 0, 0)
+        out[be.name] = [y.float().cpu(), arg.cpu(), dx.float().cpu()]
+    assert rel(out["hip"][0], out["ref"][0]) < 1e-3
+    assert rel(out["hip"][2], out["ref"][2]) < 1e-2
+
+
+def test_sgd_and_tflip(hip, ref):
+    torch.manual_seed(8)
+    n = 1000
+    w0, m0, g0 = torch.randn(n), torch.randn(n), torch.randn(n)
+    res = {}
+    for be, dev in ((ref, "cpu"), (hip, "cuda")):
+        w, m, g = w0.clone().to(dev), m0.clone().to(dev), g0.clone().to(dev)
+        wb = torch.zeros(n, dtype=torch.bfloat16 if dev == "cuda" else torch.float32, device=dev)
+        lr = torch.tensor([0.1], device=dev)
+        be.sgd_momentum(w, m, g, wb, lr, 0.9, 2e-4, 0.5)
+        res[be.name] = [w.cpu(), m.cpu(), wb.float().cpu()]
+    for a, b in zip(res["hip"], res["ref"]):
+        assert rel(a, b) < 4e-3
+    # transpose-flip
+    descs = [(0, 0, 16, 3, 3, 8), (16 * 9 * 8, 16 * 9 * 8, 32, 1, 1, 16)]
+    tot = 16 * 9 * 8 + 32 * 16
+    wflat = torch.randn(tot)
+    table, nt, total = tflip_table(descs)
+    out_ref = torch.zeros(tot)
+    ref.weight_tflip(wflat, out_ref, table, nt, total)
+    out_hip = torch.zeros(tot, dtype=torch.bfloat16, device="cuda")
+    hip.weight_tflip(bf(wflat).cuda(), out_hip, table.cuda(), nt, total)
+    torch.cuda.synchronize()
+    assert rel(out_hip, out_ref) < 1e-2
+
+
+def test_cifar_augment(hip, ref):
+    torch.manual_seed(9)
+    N = 4
+    raw = torch.randint(0, 256, (N, 32, 32, 3), dtype=torch.uint8)
+    params = torch.tensor([[0, 0, 0], [8, 8, 1], [3, 5, 1], [4, 4, 0]], dtype=torch.int32)
+    o_ref = torch.zeros(N, 32, 32, 8)
+    ref.cifar_augment(raw, params, o_ref, 4)
+    o = torch.zeros(N, 32, 32, 8, dtype=torch.bfloat16, device="cuda")
+    hip.cifar_augment(raw.cuda(), params.cuda(), o, 4)
+    torch.cuda.synchronize()
+    assert rel(o, o_ref) < 1e-2
