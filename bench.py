@@ -1,0 +1,146 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node training images/sec of ResNet-50 at bs=128 per GPU.
+
+BASELINE.json metric: "images/sec (whole node) ResNet-50 bs=128/GPU at 1/2/4/8 MI355X".
+Default config = the reference's ImageNet ResNet-v2-50 (1001 classes, 224x224, bs 128 per
+worker -> global 1024 on 8 GPUs, reference README.md:41-46), synthetic data of that shape and
+random-init weights (no datasets/checkpoints on the box). A timed step is the full training
+step: forward, backward, gradient all-reduce across ranks (RCCL), fused SGD-momentum update
+and weight-layout refresh, in bf16 compute with fp32 master weights.
+`--dataset cifar10` benchmarks the CIFAR "ResNet-50" (6n+2, n=8) instead.
+
+Launch: `python bench.py --gpus 1 --steps K --warmup W`, or for N>1
+`python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N`.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+# Reference numbers: ImageNet ResNet-50 img/s. 1 worker bs128 = 0.96 steps/s
+# (row 12, ~123 img/s); 8 workers global 1024 = 0.93 steps/s (row 8, ~952 img/s). Intermediate
+# N scale row 8's per-GPU rate. CIFAR: 1 GPU 13.94 steps/s x 128 (row 3), 4 ranks 21.82 x 128
+# (row 2), 8 ranks 28.66 x 128 (row 7).
+BASELINE_IMG_S = {
+    "imagenet": {1: 122.9, 2: 2 * 119.0, 4: 4 * 119.0, 8: 952.3},
+    "cifar10": {1: 13.94 * 128, 2: None, 4: 21.82 * 128, 8: 28.66 * 128},
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--dataset", default="imagenet", choices=["imagenet", "cifar10"])
+    ap.add_argument("--resnet_size", type=int, default=50)
+    ap.add_argument("--batch_size", type=int, default=128, help="per-GPU batch")
+    ap.add_argument("--graph", type=int, default=-1, help="capture the step in a HIP graph (-1: auto)")
+    ap.add_argument("--bucket_mb", type=float, default=25.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from distributed_resnet_tensorflow_amd.models.spec import build_spec
+    from distributed_resnet_tensorflow_amd.ops.backend import HipBackend
+    from distributed_resnet_tensorflow_amd.runtime.executor import Executor
+    from distributed_resnet_tensorflow_amd.runtime.graph import StepGraph
+    from distributed_resnet_tensorflow_amd.parallel.engine import DataParallelEngine
+
+    spec = build_spec(args.dataset, args.resnet_size)
+    be = HipBackend("cuda")
+    wd = 2e-4 if args.dataset == "cifar10" else 1e-4
+    ex = Executor(spec, args.batch_size, be, "cuda", seed=1234, weight_decay=wd)
+    eng = DataParallelEngine(ex, bucket_mb=args.bucket_mb) if world > 1 else None
+    if eng is not None:
+        eng.broadcast_parameters()
+    # synthetic data of the benchmark shape: fixed device batch (no host input pipeline)
+    be.synthetic_images(ex.images, seed=17 + rank)
+    g = torch.Generator(device="cpu").manual_seed(rank)
+    ex.labels.copy_(torch.randint(0, spec.num_classes, (args.batch_size,), generator=g, dtype=torch.int32))
+    ex.set_lr(0.1)
+
+    def step():
+        ex.forward(train=True)
+        if eng is not None:
+            eng.begin_step()
+        ex.backward()
+        if eng is not None:
+            eng.finish()
+            ex.apply_gradients(grad_scale=1.0 / world)
+        else:
+            ex.apply_gradients()
+
+    use_graph = args.graph if args.graph >= 0 else int(world == 1)
+    run = step
+    if use_graph:
+        sg = StepGraph(step, warmup=2)
+        run = sg.replay
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms = dt / args.steps * 1e3
+    img_s = args.batch_size * world * args.steps / dt
+    loss = float(ex.loss_vec.float().mean())
+    if rank == 0:
+        base = BASELINE_IMG_S.get(args.dataset, {}).get(world)
+        model = f"resnet{args.resnet_size}_v2_{args.dataset}" if args.dataset == "imagenet" else \
+            f"cifar10_resnet{args.resnet_size}_v2"
+        out = {
+            "metric": "images/sec (whole node) ResNet-50 bs=128/GPU",
+            "value": round(img_s, 2),
+            "unit": "images/sec",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "steps_per_sec": round(1e3 / ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(img_s / base, 3) if base else None,
+            "dtype": "bf16",
+            "data": "synthetic (random-init weights, fixed synthetic batch of the benchmark shape)",
+            "config": {"model": model, "global_batch": args.batch_size * world, "per_gpu_batch": args.batch_size,
+                       "image_size": spec.image_size, "num_classes": spec.num_classes,
+                       "parallelism": f"dp{world}", "hip_graph": bool(use_graph)},
+            "final_loss": round(loss, 4),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -61,6 +61,7 @@ def tflip_table(descs):
 class HipBackend:
     name = "hip"
     act_dtype = torch.bfloat16
+    acc_dtype = torch.float32
 
     def __init__(self, device="cuda"):
         self.device = torch.device(device)
@@ -280,10 +281,13 @@ class HipBackend:
 # ----------------------------------------------------------------------------------------------
 # fp32 reference backend (CPU runs + test oracle)
 # ----------------------------------------------------------------------------------------------
+_DT = [torch.float32]  # compute dtype of the reference backend (float64 for exactness tests)
+
+
 def _pre(x, in_bn, relu_in):
     if in_bn is None:
-        return x.float()
-    y = x.float() * in_bn[0].float() + in_bn[1].float()
+        return x.to(_DT[0])
+    y = x.to(_DT[0]) * in_bn[0].to(_DT[0]) + in_bn[1].to(_DT[0])
     return torch.relu(y) if relu_in else y
 
 
@@ -306,10 +310,12 @@ def _dilate(xc, dil):
 
 class RefBackend:
     name = "ref"
-    act_dtype = torch.float32
 
-    def __init__(self, device="cpu"):
+    def __init__(self, device="cpu", dtype=torch.float32):
         self.device = torch.device(device)
+        self.act_dtype = dtype
+        self.acc_dtype = dtype
+        _DT[0] = dtype
 
     def stream(self):
         return None
@@ -319,12 +325,12 @@ class RefBackend:
         _, P, Q, _ = y.shape
         xc = _dilate(_pre(x, in_bn, relu_in).permute(0, 3, 1, 2), g.dil)
         xc = _pad_for(xc, P, Q, R, S, g)
-        out = F.conv2d(xc, w.float().permute(0, 3, 1, 2), stride=g.stride).permute(0, 2, 3, 1)
+        out = F.conv2d(xc, w.to(_DT[0]).permute(0, 3, 1, 2), stride=g.stride).permute(0, 2, 3, 1)
         if residual is not None:
-            out = out + residual.float()
+            out = out + residual.to(_DT[0])
         y.copy_(out)
         if stats is not None:
-            yy = y.float().reshape(-1, K)
+            yy = y.to(_DT[0]).reshape(-1, K)
             stats.zero_()
             stats.view(-1)[:K].copy_(yy.sum(0))
             stats.view(-1)[K:2 * K].copy_((yy * yy).sum(0))
@@ -339,7 +345,7 @@ class RefBackend:
         K, R, S, C = out.shape
         _, P, Q, _ = dy.shape
         xc = _pad_for(_pre(x, in_bn, relu_in).permute(0, 3, 1, 2), P, Q, R, S, g)
-        dw = torch.nn.grad.conv2d_weight(xc, (K, C, R, S), dy.float().permute(0, 3, 1, 2), stride=g.stride)
+        dw = torch.nn.grad.conv2d_weight(xc, (K, C, R, S), dy.to(_DT[0]).permute(0, 3, 1, 2), stride=g.stride)
         out.copy_(dw.permute(0, 2, 3, 1))
 
     def bn_stats_blocks(self, M, C):
@@ -347,7 +353,7 @@ class RefBackend:
 
     def bn_stats(self, x, part):
         C = x.shape[-1]
-        xx = x.float().reshape(-1, C)
+        xx = x.to(_DT[0]).reshape(-1, C)
         part.view(-1)[:C].copy_(xx.sum(0))
         part.view(-1)[C:2 * C].copy_((xx * xx).sum(0))
         return 1
@@ -359,14 +365,14 @@ class RefBackend:
         mu = p[0] / count
         var = (p[1] / count - mu * mu).clamp_min(0)
         istd = 1.0 / torch.sqrt(var + eps)
-        scale.copy_(gamma * istd.float())
-        shift.copy_(beta - mu.float() * scale)
-        mean.copy_(mu.float())
-        invstd.copy_(istd.float())
+        scale.copy_(gamma * istd.to(_DT[0]))
+        shift.copy_(beta - mu.to(_DT[0]) * scale)
+        mean.copy_(mu.to(_DT[0]))
+        invstd.copy_(istd.to(_DT[0]))
         if update_running:
             unb = var * count / (count - 1) if count > 1 else var
-            run_mean.mul_(momentum).add_((1 - momentum) * mu.float())
-            run_var.mul_(momentum).add_((1 - momentum) * unb.float())
+            run_mean.mul_(momentum).add_((1 - momentum) * mu.to(_DT[0]))
+            run_var.mul_(momentum).add_((1 - momentum) * unb.to(_DT[0]))
 
     def bn_inference(self, gamma, beta, run_mean, run_var, eps, scale, shift, mean=None, invstd=None):
         istd = torch.rsqrt(run_var + eps)
@@ -378,21 +384,21 @@ class RefBackend:
             invstd.copy_(istd)
 
     def bn_apply(self, x, y, scale, shift, relu=True):
-        v = x.float() * scale + shift
+        v = x.to(_DT[0]) * scale + shift
         y.copy_(torch.relu(v) if relu else v)
 
     def _dy(self, dy, dpool, pool_hw, x):
         if pool_hw > 0:
             N, H, W, C = x.shape
             return (dpool.view(N, 1, 1, C) / pool_hw).expand(N, H, W, C)
-        return dy.float()
+        return dy.to(_DT[0])
 
     def bn_bwd_reduce(self, dy, dpool, pool_hw, x, scale, shift, mean, invstd, part, relu=True):
         C = x.shape[-1]
         d = self._dy(dy, dpool, pool_hw, x).reshape(-1, C)
-        xx = x.float().reshape(-1, C)
+        xx = x.to(_DT[0]).reshape(-1, C)
         if relu:
-            d = d * ((xx * scale + shift) > 0).float()
+            d = d * ((xx * scale + shift) > 0).to(_DT[0])
         xh = (xx - mean) * invstd
         part.view(-1)[:C].copy_(d.sum(0))
         part.view(-1)[C:2 * C].copy_((d * xh).sum(0))
@@ -401,28 +407,28 @@ class RefBackend:
     def bn_finalize_bwd(self, part, G, count, gamma, invstd, dgamma, dbeta, coef):
         C = gamma.numel()
         p = part.view(-1)[:G * 2 * C].view(G, 2, C).double().sum(0)
-        dbeta.copy_(p[0].float())
-        dgamma.copy_(p[1].float())
+        dbeta.copy_(p[0].to(_DT[0]))
+        dgamma.copy_(p[1].to(_DT[0]))
         coef.view(3, C)[0].copy_(gamma * invstd)
-        coef.view(3, C)[1].copy_((p[0] / count).float())
-        coef.view(3, C)[2].copy_((p[1] / count).float())
+        coef.view(3, C)[1].copy_((p[0] / count).to(_DT[0]))
+        coef.view(3, C)[2].copy_((p[1] / count).to(_DT[0]))
 
     def bn_bwd_apply(self, dy, dpool, pool_hw, x, scale, shift, mean, invstd, coef, add, dx, relu=True):
         C = x.shape[-1]
         shp = x.shape
         d = self._dy(dy, dpool, pool_hw, x).reshape(-1, C)
-        xx = x.float().reshape(-1, C)
+        xx = x.to(_DT[0]).reshape(-1, C)
         if relu:
-            d = d * ((xx * scale + shift) > 0).float()
+            d = d * ((xx * scale + shift) > 0).to(_DT[0])
         xh = (xx - mean) * invstd
         k = coef.view(3, C)
         v = k[0] * (d - k[1] - xh * k[2])
         if add is not None:
-            v = v + add.float().reshape(-1, C)
+            v = v + add.to(_DT[0]).reshape(-1, C)
         dx.copy_(v.reshape(shp))
 
     def pool_bnrelu(self, x, scale, shift, pooled, relu=True):
-        v = x.float()
+        v = x.to(_DT[0])
         if scale is not None:
             v = v * scale + shift
         if relu:
@@ -443,14 +449,14 @@ class RefBackend:
         cv.copy_(out)
 
     def softmax_xent(self, logits, labels, grad_scale, dlogits, loss, correct, probs=None):
-        lp = torch.log_softmax(logits.float(), dim=1)
+        lp = torch.log_softmax(logits.to(_DT[0]), dim=1)
         p = lp.exp()
         lab = labels.long()
         loss.copy_(-lp.gather(1, lab[:, None])[:, 0])
         if probs is not None:
             probs.copy_(p)
         if dlogits is not None:
-            oh = F.one_hot(lab, logits.shape[1]).float()
+            oh = F.one_hot(lab, logits.shape[1]).to(_DT[0])
             dlogits.copy_((p - oh) * grad_scale)
         if correct is not None:
             correct.copy_((logits.argmax(1) == lab).int())
@@ -465,7 +471,7 @@ class RefBackend:
     def maxpool_fwd(self, x, y, arg, k, stride, pad_h, pad_w):
         N, H, W, C = x.shape
         _, P, Q, _ = y.shape
-        xc = x.float().permute(0, 3, 1, 2)
+        xc = x.to(_DT[0]).permute(0, 3, 1, 2)
         pb = (P - 1) * stride + k - pad_h - H
         pr = (Q - 1) * stride + k - pad_w - W
         xp = F.pad(xc, (pad_w, pr, pad_h, pb), value=float("-inf"))
@@ -480,12 +486,12 @@ class RefBackend:
         _, P, Q, _ = dy.shape
         Hp = (P - 1) * stride + k
         Wp = (Q - 1) * stride + k
-        acc = torch.zeros(N, max(Hp, H + pad_h), max(Wp, W + pad_w), C, dtype=torch.float32)
+        acc = torch.zeros(N, max(Hp, H + pad_h), max(Wp, W + pad_w), C, dtype=_DT[0])
         a = arg.long()
-        d = dy.float()
+        d = dy.to(_DT[0])
         for r in range(k):
             for s in range(k):
-                m = (a == r * k + s).float() * d
+                m = (a == r * k + s).to(_DT[0]) * d
                 acc[:, r:r + (P - 1) * stride + 1:stride, s:s + (Q - 1) * stride + 1:stride, :] += m
         dx.copy_(acc[:, pad_h:pad_h + H, pad_w:pad_w + W, :])
 
@@ -514,8 +520,8 @@ class RefBackend:
 
     def cifar_augment(self, raw_u8, params_i32, out, pad):
         N, H, W, _ = raw_u8.shape
-        img = raw_u8.float()
-        res = torch.zeros(N, H, W, out.shape[-1])
+        img = raw_u8.to(_DT[0])
+        res = torch.zeros(N, H, W, out.shape[-1], dtype=_DT[0])
         for n in range(N):
             oy, ox, flip = [int(v) for v in params_i32[n].tolist()]
             padded = F.pad(img[n].permute(2, 0, 1), (pad, pad, pad, pad))

@@ -1,0 +1,130 @@
+"""Data-parallel engine: bucketed gradient all-reduce overlapped with the backward pass.
+
+Replaces both distribution strategies of the reference:
+  * SyncReplicasOptimizer over parameter servers (resnet_model.py:101-112, CS1-CS3): every
+    worker pushes gradients to PS accumulators, the chief averages N of them and applies
+    Momentum. Mathematically that is "average the N replicas' gradients, then every replica
+    applies the same update" -- which is exactly an all-reduce(mean) + identical local SGD, with
+    no PS process and no per-step variable fetch.
+  * Horovod DistributedOptimizer (resnet_model.py:114-116) + BroadcastGlobalVariablesHook(0)
+    (resnet_cifar_main_horovod.py:316): same all-reduce, plus a rank-0 broadcast at start.
+
+MI355X design: one process per GPU, torch.distributed "nccl" (= RCCL over xGMI). The flat
+gradient buffer (runtime/params.py) is cut into contiguous buckets in REVERSE creation order;
+the executor reports, after every residual block's backward, the lowest flat offset whose
+gradients are complete, and every bucket that is fully complete is all-reduced immediately
+(async op on RCCL's stream, ordered after the producing kernels) while earlier blocks are still
+back-propagating. `finish()` makes the compute stream wait for the last bucket before the
+fused SGD launch. The average's 1/N is folded into the SGD kernel (grad_scale). Bucket size
+default 25 MB: ResNet-50's 102 MB of fp32 gradients -> 5 buckets, each large enough to run
+RCCL at link bandwidth on the 7 point-to-point xGMI links of an 8-GPU node and small enough
+that only the last (smallest-layer) bucket is exposed after backward.
+
+Async PS training (--sync_replicas=False with --job_name set) maps to
+`mode="delayed"`: step t applies the averaged gradient of step t-1 while step t's all-reduce
+runs behind step t+1's compute (bounded staleness 1, no PS).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+class DataParallelEngine:
+    def __init__(self, executor, bucket_mb: float = 25.0, mode: str = "sync", group=None):
+        self.ex = executor
+        self.P = executor.P
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.mode = mode
+        self.buckets = self._make_buckets(int(bucket_mb * (1 << 20) // 4))
+        self.works: List = []
+        self.launched = [False] * len(self.buckets)
+        self.frontier = self.P.total
+        self._delayed_pending = False
+        if mode == "delayed":
+            self.comm_grad = torch.zeros_like(self.P.grad)
+            self.ready_grad = torch.zeros_like(self.P.grad)
+
+    # -- bucket layout ---------------------------------------------------------------------------
+    def _make_buckets(self, cap_elems: int):
+        """Contiguous [lo, hi) slices from the END of the flat buffer, cut at slot boundaries."""
+        bounds = [s.offset for s in self.P.slots] + [self.P.total]
+        buckets = []
+        hi = self.P.total
+        for i in range(len(bounds) - 2, -1, -1):
+            lo = bounds[i]
+            if hi - lo >= cap_elems and lo != hi:
+                buckets.append((lo, hi))
+                hi = lo
+        if hi > 0:
+            buckets.append((0, hi))
+        return buckets  # ordered from the end of the buffer (first ready) to the start
+
+    # -- hooks --------------------------------------------------------------------------------------
+    def begin_step(self):
+        self.works = []
+        self.launched = [False] * len(self.buckets)
+        self.frontier = self.P.total
+        if self.mode == "sync":
+            self.ex.grad_ready = self._on_ready
+        else:
+            self.ex.grad_ready = None
+
+    def _launch(self, i: int, buf: Optional[torch.Tensor] = None):
+        lo, hi = self.buckets[i]
+        t = (self.P.grad if buf is None else buf)[lo:hi]
+        self.works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        self.launched[i] = True
+
+    def _on_ready(self, lo_ready: int):
+        self.frontier = min(self.frontier, lo_ready)
+        for i, (lo, hi) in enumerate(self.buckets):
+            if not self.launched[i] and lo >= self.frontier:
+                self._launch(i)
+
+    def finish(self) -> torch.Tensor:
+        """Complete the step's gradient exchange; returns the gradient buffer SGD must use."""
+        if self.mode == "sync":
+            for i in range(len(self.buckets)):
+                if not self.launched[i]:
+                    self._launch(i)
+            for w in self.works:
+                w.wait()
+            self.works = []
+            self.ex.grad_ready = None
+            return self.P.grad
+        # delayed (async-PS analog): finish last step's exchange, start this step's
+        for w in self.works:
+            w.wait()
+        self.works = []
+        had = self._delayed_pending
+        if had:
+            self.ready_grad.copy_(self.comm_grad)
+        else:
+            self.ready_grad.zero_()
+        self.comm_grad.copy_(self.P.grad)
+        for i in range(len(self.buckets)):
+            self._launch(i, self.comm_grad)
+        self._delayed_pending = True
+        return self.ready_grad
+
+    # -- state sync -----------------------------------------------------------------------------------
+    def broadcast_parameters(self, src: int = 0):
+        """Rank-0 broadcast of every variable (Horovod BroadcastGlobalVariablesHook(0) analog)."""
+        for t in (self.P.master, self.P.momentum, self.P.bn_state):
+            dist.broadcast(t, src=src, group=self.group)
+        step = torch.tensor([self.P.global_step], dtype=torch.int64,
+                            device=self.P.master.device)
+        dist.broadcast(step, src=src, group=self.group)
+        self.P.global_step = int(step.item())
+        self.ex.sync_weights()
+
+    def average_bn_state(self):
+        """Optional: average BN moving statistics before checkpoint/eval (the reference keeps them
+        per replica and checkpoints the chief's copy, so this is off by default)."""
+        dist.all_reduce(self.P.bn_state, op=dist.ReduceOp.SUM, group=self.group)
+        self.P.bn_state.div_(self.world)

@@ -1,0 +1,412 @@
+"""Static-plan training executor for ResNet v2 on the gfx950 kernel library.
+
+This is the analog of the TF1 C++ graph executor the reference runs each
+``mon_sess.run(train_op)`` (resnet_cifar_main.py:320-321): one training step =
+forward + hand-derived backward + fused SGD-momentum, issued as a fixed sequence of kernel
+launches over PRE-ALLOCATED buffers (so the whole step is capturable as one HIP graph,
+runtime/graph.py). There is no autograd tape: the backward of the pre-activation network is
+written out explicitly, which is what lets BatchNorm/ReLU be fused across kernel boundaries:
+
+  forward, per conv: y = conv( relu(bn(x)) ) [+ shortcut]   -- BN-apply+ReLU in the load
+      prologue of the consuming conv (the normalised activation is never written to HBM),
+      residual add + the NEXT BN's partial statistics in the epilogue of the producing conv.
+  backward, per conv: dgrad as a forward conv of dY with flipped/transposed weights (the
+      projection-shortcut dgrad accumulates through the residual epilogue), wgrad recomputes
+      relu(bn(x)) in its load prologue, BN-ReLU backward = reduce -> finalize -> apply (+ the
+      identity-shortcut gradient fused into the apply).
+
+Gradients land directly in the flat gradient buffer (runtime/params.py) in reverse creation
+order; ``grad_ready`` callbacks report the completed suffix so the data-parallel engine can
+start bucket all-reduces while earlier layers are still back-propagating.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, List, Optional
+
+import torch
+
+from ..models.spec import Block, BN, Conv, NetSpec
+from ..ops.backend import ConvGeom, dgrad_geom, tflip_table
+from .params import ParamStore
+
+BN_DECAY = 0.997     # reference resnet_model_official.py:37
+BN_EPSILON = 1e-5    # reference resnet_model_official.py:38
+
+
+@dataclass
+class BNState:
+    bn: BN
+    gamma: torch.Tensor
+    beta: torch.Tensor
+    dgamma: torch.Tensor
+    dbeta: torch.Tensor
+    run_mean: torch.Tensor
+    run_var: torch.Tensor
+    scale: torch.Tensor
+    shift: torch.Tensor
+    mean: torch.Tensor
+    invstd: torch.Tensor
+    stats: Optional[torch.Tensor] = None  # partial stats of the normalised tensor [G][2][C]
+    G: int = 1
+    rows: int = 0                          # N*H*W of the normalised tensor
+
+    @property
+    def ss(self):
+        return (self.scale, self.shift)
+
+
+@dataclass
+class ConvOp:
+    conv: Conv
+    geom: ConvGeom
+    w: torch.Tensor        # compute weights [K,R,S,C]
+    wt: Optional[torch.Tensor]  # dgrad weights [C,R,S,K]
+    dw: torch.Tensor       # fp32 grad view [K,R,S,C]
+    grad_lo: int           # flat offset of this conv's gradient slot
+
+
+@dataclass
+class BlockPlan:
+    blk: Block
+    x: torch.Tensor                 # block input (raw residual stream)
+    bn: List[BNState]               # [bn1, bn2(, bn3)]
+    convs: List[ConvOp]             # main path
+    proj: Optional[ConvOp]
+    hs: List[torch.Tensor]          # raw conv outputs of the main path except the last
+    sc: Optional[torch.Tensor]      # projection output
+    out: torch.Tensor               # block output
+    grad_lo: int                    # lowest flat grad offset written by this block
+
+
+class Executor:
+    def __init__(self, spec: NetSpec, batch: int, backend, device, seed: int = 0,
+                 weight_decay: float = 2e-4, momentum: float = 0.9, params: ParamStore | None = None):
+        self.spec, self.N, self.be = spec, batch, backend
+        self.device = torch.device(device)
+        self.wd, self.mom = weight_decay, momentum
+        self.is_hip = backend.name == "hip"
+        self.fdt = backend.acc_dtype
+        self.P = params or ParamStore(spec, self.device, keep_bf16=self.is_hip, seed=seed, dtype=self.fdt)
+        self.grad_ready: Optional[Callable[[int], None]] = None
+        self._alloc()
+        self.sync_weights()
+
+    # ------------------------------------------------------------------------------------------
+    # allocation
+    # ------------------------------------------------------------------------------------------
+    def _act(self, *shape):
+        return torch.zeros(*shape, dtype=self.be.act_dtype, device=self.device)
+
+    def _f32(self, *shape):
+        return torch.zeros(*shape, dtype=self.fdt, device=self.device)
+
+    def _bn_state(self, bn: BN) -> BNState:
+        P = self.P
+        rm, rv = P.moving(bn.name)
+        return BNState(bn, P.w(f"{bn.name}/gamma"), P.w(f"{bn.name}/beta"), P.g(f"{bn.name}/gamma"),
+                       P.g(f"{bn.name}/beta"), rm, rv, self._f32(bn.c), self._f32(bn.c), self._f32(bn.c),
+                       self._f32(bn.c))
+
+    def _conv_op(self, c: Conv, wt_descs, wt_off) -> tuple[ConvOp, int]:
+        P = self.P
+        name = f"{c.name}/kernel"
+        s = P.by_name[name]
+        g = ConvGeom(c.stride, c.pad, c.pad, 1)
+        wt = None
+        if c is not self.spec.stem:
+            wt_descs.append((s.offset, wt_off, c.cout, c.k, c.k, c.cin_store))
+            wt = (c.cin_store, c.k, c.k, c.cout)
+            wt_off += s.numel
+        op = ConvOp(c, g, P.compute_w(name), wt, P.g(name), s.offset)
+        return op, wt_off
+
+    def _stats_for(self, M: int, C: int) -> tuple[torch.Tensor, int]:
+        G = self.be.conv_stats_tiles(M, C)
+        return self._f32(G, 2, C), G
+
+    def _alloc(self):
+        sp, N = self.spec, self.N
+        be = self.be
+        wt_descs, wt_off = [], 0
+        self.stem_op, wt_off = self._conv_op(sp.stem, wt_descs, wt_off)
+        img = sp.image_size
+        self.images = self._act(N, img, img, sp.stem.cin_store)
+        self.labels = torch.zeros(N, dtype=torch.int32, device=self.device)
+        hs = sp.stem_hw
+        self.stem_out = self._act(N, hs, hs, sp.stem.cout)
+        max_act = N * hs * hs * sp.stem.cout
+        max_bn_part = 0
+        if sp.maxpool:
+            ph = sp.pool_hw
+            self.pool_out = self._act(N, ph, ph, sp.stem.cout)
+            self.pool_arg = torch.zeros(N, ph, ph, sp.stem.cout, dtype=torch.uint8, device=self.device)
+            Gp = be.bn_stats_blocks(N * ph * ph, sp.stem.cout)
+            self.pool_stats, self.pool_G = self._f32(Gp, 2, sp.stem.cout), Gp
+            x, x_stats, x_G = self.pool_out, self.pool_stats, self.pool_G
+            self.stem_stats, self.stem_G = None, 0
+        else:
+            self.stem_stats, self.stem_G = self._stats_for(N * hs * hs, sp.stem.cout)
+            x, x_stats, x_G = self.stem_out, self.stem_stats, self.stem_G
+        self.blocks: List[BlockPlan] = []
+        ws_need = be.wgrad_ws_elems(N * hs * hs, sp.stem.cout, sp.stem.k, sp.stem.k, sp.stem.cin_store)
+        for blk in sp.blocks:
+            bns = [self._bn_state(blk.bn1)] + [self._bn_state(b) for b in blk.bns]
+            bns[0].stats, bns[0].G = x_stats, x_G
+            bns[0].rows = x.numel() // blk.in_c
+            convs = []
+            for c in blk.convs:
+                op, wt_off = None, wt_off
+                op, wt_off = self._conv_op(c, wt_descs, wt_off)
+                convs.append(op)
+            proj = None
+            if blk.proj is not None:
+                proj, wt_off = self._conv_op(blk.proj, wt_descs, wt_off)
+            # main-path intermediate outputs + their stats (feeding bn2/bn3)
+            h_list = []
+            hw = blk.in_hw
+            for i, c in enumerate(blk.convs[:-1]):
+                hw = c.out_hw(hw)
+                h = self._act(N, hw, hw, c.cout)
+                st, G = self._stats_for(N * hw * hw, c.cout)
+                bns[i + 1].stats, bns[i + 1].G = st, G
+                bns[i + 1].rows = N * hw * hw
+                h_list.append(h)
+                max_act = max(max_act, h.numel())
+            ohw = blk.out_hw
+            out = self._act(N, ohw, ohw, blk.out_c)
+            sc = self._act(N, ohw, ohw, blk.out_c) if proj is not None else None
+            max_act = max(max_act, out.numel(), x.numel())
+            grad_lo = min([o.grad_lo for o in convs] + ([proj.grad_lo] if proj else []) +
+                          [self.P.by_name[f"{b.bn.name}/gamma"].offset for b in bns])
+            bp = BlockPlan(blk, x, bns, convs, proj, h_list, sc, out, grad_lo)
+            self.blocks.append(bp)
+            out_stats, out_G = self._stats_for(N * ohw * ohw, blk.out_c)
+            bp.out_stats, bp.out_G = out_stats, out_G
+            # wgrad workspaces
+            hw = blk.in_hw
+            ins = [x] + h_list
+            for op, xin in zip(convs, ins):
+                o_hw = op.conv.out_hw(xin.shape[1])
+                ws_need = max(ws_need, be.wgrad_ws_elems(N * o_hw * o_hw, op.conv.cout, op.conv.k, op.conv.k,
+                                                         op.conv.cin_store))
+            if proj is not None:
+                ws_need = max(ws_need, be.wgrad_ws_elems(N * ohw * ohw, proj.conv.cout, 1, 1, proj.conv.cin_store))
+            x, x_stats, x_G = out, out_stats, out_G
+        # head
+        self.final_bn = self._bn_state(sp.final_bn)
+        self.final_bn.stats, self.final_bn.G = x_stats, x_G
+        self.final_bn.rows = x.numel() // sp.final_c
+        self.last_out = x
+        C, ncls = sp.final_c, sp.num_classes
+        self.pooled = self._f32(N, C)
+        self.logits = self._f32(N, ncls)
+        self.dlogits = self._f32(N, ncls)
+        self.loss_vec = self._f32(N)
+        self.correct = torch.zeros(N, dtype=torch.int32, device=self.device)
+        self.dpool = self._f32(N, C)
+        self.dense_w = self.P.w(f"{sp.dense_name}/kernel")
+        self.dense_b = self.P.w(f"{sp.dense_name}/bias")
+        self.dense_dw = self.P.g(f"{sp.dense_name}/kernel")
+        self.dense_db = self.P.g(f"{sp.dense_name}/bias")
+        # backward scratch (stream-ordered reuse)
+        self.g_a = self._act(max_act)
+        self.g_b = self._act(max_act)
+        self.g_c = self._act(max_act)
+        part = 0
+        for b in [bb for bp in self.blocks for bb in bp.bn] + [self.final_bn]:
+            M = b.rows
+            part = max(part, be.bn_stats_blocks(M, b.bn.c) * 2 * b.bn.c)
+        self.bn_part = self._f32(max(part, 16))
+        self.bn_coef = self._f32(3 * max(b.bn.c for bp in self.blocks for b in bp.bn + [self.final_bn]))
+        self.wgrad_ws = self._f32(max(ws_need, 16))
+        # data-gradient weights (flipped / channel-transposed), one flat buffer + device table
+        self.wt_flat = torch.zeros(max(wt_off, 16), dtype=self.be.act_dtype, device=self.device)
+        self.wt_descs = wt_descs
+        table, nt, total = tflip_table(wt_descs)
+        self.wt_table, self.wt_n, self.wt_total = table.to(self.device), nt, total
+        for op in self._all_ops():
+            if op.wt is not None:
+                src = self.P.by_name[f"{op.conv.name}/kernel"].offset
+                d = next(d for d in wt_descs if d[0] == src)
+                op.wt = self.wt_flat[d[1]:d[1] + op.dw.numel()].view(op.wt)
+        self.lr_t = self._f32(1)
+
+    def _all_ops(self):
+        yield self.stem_op
+        for bp in self.blocks:
+            yield from bp.convs
+            if bp.proj is not None:
+                yield bp.proj
+
+    # ------------------------------------------------------------------------------------------
+    # weights
+    # ------------------------------------------------------------------------------------------
+    def sync_weights(self):
+        """Refresh the compute copies (bf16 + flipped dgrad weights) from the fp32 master."""
+        if self.P.wbf16 is not None:
+            self.be.cast_bf16(self.P.master, self.P.wbf16)
+        src = self.P.wbf16 if self.P.wbf16 is not None else self.P.master
+        if self.wt_n:
+            if self.is_hip:
+                self.be.weight_tflip(src, self.wt_flat, self.wt_table, self.wt_n, self.wt_total)
+            else:
+                self.be.weight_tflip(src, self.wt_flat, self.wt_table.cpu(), self.wt_n, self.wt_total)
+
+    # ------------------------------------------------------------------------------------------
+    # forward
+    # ------------------------------------------------------------------------------------------
+    def _bn_fwd(self, b: BNState, train: bool):
+        if train:
+            self.be.bn_finalize(b.stats, b.G, b.rows, b.gamma, b.beta, b.run_mean, b.run_var, b.scale, b.shift,
+                                b.mean, b.invstd, BN_DECAY, BN_EPSILON, update_running=True)
+        else:
+            self.be.bn_inference(b.gamma, b.beta, b.run_mean, b.run_var, BN_EPSILON, b.scale, b.shift, b.mean,
+                                 b.invstd)
+
+    def forward(self, train: bool = True):
+        """Runs the network on self.images/self.labels; fills loss_vec/correct (and dlogits)."""
+        be, sp = self.be, self.spec
+        st = self.stem_op
+        be.conv_fwd(self.images, st.w, self.stem_out, st.geom, stats=self.stem_stats if train else None)
+        if sp.maxpool:
+            ph = sp.pool_hw
+            pad = max((ph - 1) * 2 + 3 - sp.stem_hw, 0) // 2
+            be.maxpool_fwd(self.stem_out, self.pool_out, self.pool_arg, 3, 2, pad, pad)
+            if train:
+                be.bn_stats(self.pool_out, self.pool_stats)
+        for bp in self.blocks:
+            self._block_fwd(bp, train)
+        fb = self.final_bn
+        self._bn_fwd(fb, train)
+        be.pool_bnrelu(self.last_out, fb.scale, fb.shift, self.pooled, relu=True)
+        N, C, ncls = self.N, sp.final_c, sp.num_classes
+        be.sgemm(0, 1, N, ncls, C, 1.0, self.pooled, C, self.dense_w, C, 0.0, self.logits, ncls, bias=self.dense_b)
+        be.softmax_xent(self.logits, self.labels, 1.0 / N, self.dlogits if train else None, self.loss_vec,
+                        self.correct)
+
+    def _block_fwd(self, bp: BlockPlan, train: bool):
+        be = self.be
+        bn = bp.bn
+        self._bn_fwd(bn[0], train)
+        if bp.proj is not None:
+            be.conv_fwd(bp.x, bp.proj.w, bp.sc, bp.proj.geom, in_bn=bn[0].ss)
+        inp = bp.x
+        for i, op in enumerate(bp.convs):
+            last = i == len(bp.convs) - 1
+            if last:
+                res = bp.sc if bp.proj is not None else bp.x
+                be.conv_fwd(inp, op.w, bp.out, op.geom, in_bn=bn[i].ss, residual=res,
+                            stats=bp.out_stats if train else None)
+            else:
+                be.conv_fwd(inp, op.w, bp.hs[i], op.geom, in_bn=bn[i].ss,
+                            stats=bn[i + 1].stats if train else None)
+                self._bn_fwd(bn[i + 1], train)
+                inp = bp.hs[i]
+
+    # ------------------------------------------------------------------------------------------
+    # backward
+    # ------------------------------------------------------------------------------------------
+    def _view(self, buf, like):
+        return buf[:like.numel()].view(like.shape)
+
+    def _bn_bwd(self, b: BNState, x, dy, dx, add=None, dpool=None, pool_hw=0):
+        """dx = BN-ReLU backward of (x -> relu(bn(x))) given dy = d/d relu-output; + add."""
+        be = self.be
+        M = x.numel() // b.bn.c
+        part = self.bn_part
+        G = be.bn_bwd_reduce(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, part)
+        coef = self.bn_coef[:3 * b.bn.c]
+        be.bn_finalize_bwd(part, G, M, b.gamma, b.invstd, b.dgamma, b.dbeta, coef)
+        be.bn_bwd_apply(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, coef, add, dx)
+
+    def backward(self):
+        be, sp = self.be, self.spec
+        N, C, ncls = self.N, sp.final_c, sp.num_classes
+        # dense layer
+        be.sgemm(1, 0, ncls, C, N, 1.0, self.dlogits, ncls, self.pooled, C, 0.0, self.dense_dw, C)
+        be.colsum(self.dlogits, self.dense_db)
+        be.sgemm(0, 0, N, C, ncls, 1.0, self.dlogits, ncls, self.dense_w, C, 0.0, self.dpool, C)
+        fb = self.final_bn
+        hw = self.last_out.shape[1] * self.last_out.shape[2]
+        d_out = self._view(self.g_a, self.last_out)
+        self._bn_bwd(fb, self.last_out, None, d_out, dpool=self.dpool, pool_hw=hw)
+        if self.grad_ready is not None:
+            self.grad_ready(self.P.by_name[f"{fb.bn.name}/gamma"].offset)
+        bufs = [self.g_a, self.g_b, self.g_c]
+        cur = 0  # index of the buffer holding d_out
+        for bp in reversed(self.blocks):
+            cur = self._block_bwd(bp, bufs, cur)
+            if self.grad_ready is not None:
+                self.grad_ready(bp.grad_lo)
+        d_x0 = self._view(bufs[cur], self.blocks[0].x)
+        st = self.stem_op
+        if sp.maxpool:
+            d_stem = self._view(bufs[(cur + 1) % 3], self.stem_out)
+            ph = sp.pool_hw
+            pad = max((ph - 1) * 2 + 3 - sp.stem_hw, 0) // 2
+            be.maxpool_bwd(d_x0, self.pool_arg, d_stem, 3, 2, pad, pad)
+        else:
+            d_stem = d_x0
+        be.conv_wgrad(self.images, d_stem, st.dw, st.geom, ws=self.wgrad_ws)
+        if self.grad_ready is not None:
+            self.grad_ready(0)
+
+    def _block_bwd(self, bp: BlockPlan, bufs, cur: int) -> int:
+        """Back-propagates one block; bufs[cur] holds d(block output). Returns the index of the
+        buffer holding d(block input). Two free buffers alternate: the dgrad of conv i writes the
+        one not holding its dY, and the BN-ReLU backward then runs in place on it."""
+        be = self.be
+        d_out = self._view(bufs[cur], bp.out)
+        free = [bufs[(cur + 1) % 3], bufs[(cur + 2) % 3]]
+        ins = [bp.x] + bp.hs                 # raw inputs of each main-path conv
+        dy, dy_buf = d_out, bufs[cur]
+        for i in reversed(range(len(bp.convs))):
+            op, xin, b = bp.convs[i], ins[i], bp.bn[i]
+            tgt = free[0] if dy_buf is not free[0] else free[1]
+            be.conv_wgrad(xin, dy, op.dw, op.geom, in_bn=b.ss, ws=self.wgrad_ws)
+            da = self._view(tgt, xin)        # d relu(bn(xin))
+            be.conv_fwd(dy, op.wt, da, dgrad_geom(op.geom, op.conv.k, op.conv.k))
+            add = None
+            if i == 0:
+                if bp.proj is not None:
+                    pj = bp.proj
+                    be.conv_wgrad(bp.x, d_out, pj.dw, pj.geom, in_bn=b.ss, ws=self.wgrad_ws)
+                    be.conv_fwd(d_out, pj.wt, da, dgrad_geom(pj.geom, 1, 1), residual=da)
+                else:
+                    add = d_out              # identity shortcut
+            self._bn_bwd(b, xin, da, da, add=add)
+            dy, dy_buf = da, tgt
+        return next(k for k, t in enumerate(bufs) if t is dy_buf)
+
+    # ------------------------------------------------------------------------------------------
+    # optimizer
+    # ------------------------------------------------------------------------------------------
+    def set_lr(self, lr: float):
+        self.lr_t.fill_(float(lr))
+
+    def apply_gradients(self, grad_scale: float = 1.0):
+        P = self.P
+        self.be.sgd_momentum(P.master, P.momentum, P.grad, P.wbf16, self.lr_t, self.mom, self.wd, grad_scale)
+        if self.wt_n:
+            src = P.wbf16 if P.wbf16 is not None else P.master
+            table = self.wt_table if self.is_hip else self.wt_table.cpu()
+            self.be.weight_tflip(src, self.wt_flat, table, self.wt_n, self.wt_total)
+
+    def train_step(self, lr: Optional[float] = None, grad_scale: float = 1.0, allreduce: Optional[Callable] = None):
+        if lr is not None:
+            self.set_lr(lr)
+        self.forward(train=True)
+        self.backward()
+        if allreduce is not None:
+            allreduce()
+        self.apply_gradients(grad_scale)
+
+    # ------------------------------------------------------------------------------------------
+    # metrics (host side, off the hot path)
+    # ------------------------------------------------------------------------------------------
+    def metrics(self) -> dict:
+        xent = float(self.loss_vec.double().mean())
+        prec = float(self.correct.double().mean())
+        l2 = float(self.P.trainable_l2())
+        return {"cross_entropy": xent, "cost": xent + self.wd * l2, "precision": prec}

@@ -1,0 +1,63 @@
+"""The static-plan executor's hand-written backward equals autograd of the oracle network.
+
+Runs the executor on the fp32/fp64 reference backend (CPU) so the comparison isolates the
+executor's plan (layer order, BN/ReLU fusion boundaries, shortcut gradients, buffer reuse)
+from kernel rounding; the GPU tests compare each HIP kernel against the same backend.
+"""
+import pytest
+import torch
+
+from distributed_resnet_tensorflow_amd.models import oracle
+from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2, imagenet_resnet_v2
+from distributed_resnet_tensorflow_amd.ops.backend import RefBackend
+from distributed_resnet_tensorflow_amd.runtime.executor import Executor
+
+
+def _check(spec, N, dtype, tol):
+    torch.manual_seed(0)
+    ex = Executor(spec, N, RefBackend(dtype=dtype), "cpu", seed=1)
+    ex.images.zero_()
+    ex.images[..., :3] = torch.randn(N, spec.image_size, spec.image_size, 3, dtype=dtype)
+    labels = torch.randint(0, spec.num_classes, (N,))
+    ex.labels.copy_(labels.int())
+    p = oracle.params_from_store(ex.P)
+    st = oracle.state_from_store(ex.P)
+    ex.forward(train=True)
+    ex.backward()
+    logits, xent, _ = oracle.loss_fn(spec, p, st, ex.images, labels)
+    xent.backward()
+    assert torch.allclose(logits, ex.logits, atol=tol * 10, rtol=tol * 10)
+    assert abs(xent.item() - ex.loss_vec.mean().item()) < tol * 10
+    for s in ex.P.slots:
+        g_ex = ex.P.to_tf(s.name, buf=ex.P.grad, dtype=dtype)
+        g_or = p[s.name].grad
+        err = ((g_ex - g_or).norm() / (g_or.norm() + 1e-30)).item()
+        assert err < tol, (s.name, err)
+    for k in st:
+        m, v = ex.P.moving(k)
+        assert torch.allclose(m, st[k][0], atol=tol) and torch.allclose(v, st[k][1], atol=tol * 10)
+
+
+def test_cifar_resnet8_fp32():
+    _check(cifar_resnet_v2(8), 4, torch.float32, 1e-4)
+
+
+def test_imagenet_resnet18_fp32():
+    _check(imagenet_resnet_v2(18, num_classes=10, image_size=64), 2, torch.float32, 1e-4)
+
+
+def test_imagenet_resnet50_fp64():
+    _check(imagenet_resnet_v2(50, num_classes=7, image_size=64), 2, torch.float64, 1e-9)
+
+
+def test_sgd_step_matches_torch_momentum():
+    spec = cifar_resnet_v2(8)
+    ex = Executor(spec, 2, RefBackend(), "cpu", seed=3, weight_decay=2e-4, momentum=0.9)
+    w0 = ex.P.master.clone()
+    ex.P.grad.normal_()
+    g = ex.P.grad.clone()
+    ex.set_lr(0.1)
+    ex.apply_gradients(grad_scale=0.5)
+    m = g * 0.5 + 2e-4 * w0
+    assert torch.allclose(ex.P.master, w0 - 0.1 * m, atol=1e-6)
+    assert torch.allclose(ex.P.momentum, m, atol=1e-6)

@@ -164,6 +164,32 @@ def test_bn_forward_and_backward(hip, ref, C):
         assert rel(a, b) < 1e-2
 
 
+def test_bn_backward_pool_broadcast(hip, ref):
+    """Final-BN backward with dY = dpool / HW broadcast (the global-average-pool gradient)."""
+    torch.manual_seed(10)
+    N, H, C = 4, 7, 256
+    x = bf(torch.randn(N, H, H, C))
+    dpool = torch.randn(N, C)
+    gamma, beta = torch.rand(C) + 0.5, torch.randn(C) * 0.2
+    outs = {}
+    for be, dev in ((ref, "cpu"), (hip, "cuda")):
+        xx = x.to(dev) if dev == "cuda" else x.float()
+        part = torch.zeros(be.bn_stats_blocks(N * H * H, C), 2, C, device=dev)
+        G = be.bn_stats(xx, part)
+        sc, sh, mu, isd = (torch.zeros(C, device=dev) for _ in range(4))
+        be.bn_finalize(part, G, N * H * H, gamma.to(dev), beta.to(dev), None, None, sc, sh, mu, isd, 0.997, 1e-5,
+                       update_running=False)
+        partb = torch.zeros(be.bn_stats_blocks(N * H * H, C), 2, C, device=dev)
+        Gb = be.bn_bwd_reduce(None, dpool.to(dev), H * H, xx, sc, sh, mu, isd, partb)
+        dg, db, coef = torch.zeros(C, device=dev), torch.zeros(C, device=dev), torch.zeros(3 * C, device=dev)
+        be.bn_finalize_bwd(partb, Gb, N * H * H, gamma.to(dev), isd, dg, db, coef)
+        dx = torch.zeros_like(xx)
+        be.bn_bwd_apply(None, dpool.to(dev), H * H, xx, sc, sh, mu, isd, coef, None, dx)
+        outs[be.name] = [t.float().cpu() for t in (dg, db, dx)]
+    for a, b in zip(outs["hip"], outs["ref"]):
+        assert rel(a, b) < 1e-2
+
+
 def test_bn_autograd_oracle(ref):
     """The hand-written BN-ReLU backward equals autograd of batch-norm + relu (CPU oracle)."""
     torch.manual_seed(5)
