@@ -23,7 +23,7 @@ struct DrnConvFwdArgs {
   const float* in_scale;  // optional [C]: fused BN apply on the input: relu(x*scale+shift)
   const float* in_shift;  // optional [C]
   const void* residual;   // optional bf16 [N][P][Q][K]: y = conv + residual
-  float* stats;           // optional [tiles_p][2][K]: per-pixel-tile partial sum / sumsq of y
+  float* stats;           // optional [2][K] fp32 accumulator (+= sum, sumsq of y); pre-zeroed
   int32_t N, H, W, C, K, R, S, P, Q;
   int32_t stride, pad_h, pad_w, dil;
   int32_t relu_in;        // 1: relu after the fused scale/shift

@@ -4,20 +4,23 @@
 // `batch_norm_relu` (reference resnet_model_official.py:41-50: momentum 0.997, eps 1e-5,
 // center+scale, per-replica statistics, moving averages via UPDATE_OPS, resnet_model.py:119).
 //
-// Statistics flow (all deterministic, no float atomics):
-//   forward  : partial sums  -> drn_bn_finalize -> scale/shift (+ running stats update)
-//              partial sums come either from drn_bn_stats or straight from the producing
-//              convolution's epilogue (conv_fwd.hip `stats`), in the same [G][2][C] layout;
-//              scale/shift are then applied inside the CONSUMER conv's load prologue.
+// Statistics flow: every reduction ends in a [2][C] fp32 accumulator (per-block register/LDS
+// reduction, then ONE atomic add per channel per block); the finalize kernels read it and zero
+// it again for the next step, so no memset is replayed and the finalize is C threads of O(1).
+//   forward  : sums -> drn_bn_finalize -> scale/shift (+ running stats update); the sums come
+//              from drn_bn_stats or straight from the producing convolution's epilogue
+//              (conv_fwd.hip `stats`); scale/shift are then applied inside the CONSUMER conv's
+//              load prologue.
 //   backward : drn_bn_bwd_reduce (sum g, sum g*xhat, g = dy * relu'(y)) -> drn_bn_finalize_bwd
 //              (dgamma/dbeta into the gradient buffer + per-channel coefficients)
 //              -> drn_bn_bwd_apply (dx, optionally + the identity-shortcut gradient).
+// fp32 atomics make the statistics order-nondeterministic in the last bits (like cuDNN's).
 // Every kernel reads/writes 16-byte vectors (8 channels) per lane.
 #include "drn_common.h"
 
 namespace drn {
 
-// x [M][C] -> part[blockIdx][2][C]
+// x [M][C] -> acc[2][C] += (sum, sumsq)
 __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ x, float* __restrict__ part, int M,
                                                        int C, int rows_per_block) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -56,23 +59,22 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict_
     const int cvv = c / 8, j = c % 8;
     float acc = 0.f;
     for (int r = 0; r < rpp; ++r) acc += red[(r * CV + cvv) * 16 + which * 8 + j];
-    part[((size_t)blockIdx.x * 2 + which) * C + c] = acc;
+    atomicAdd(part + (size_t)which * C + c, acc);
   }
 }
 
-// part[G][2][C] -> scale/shift (+mean, invstd), running stats update. One thread per channel.
-__global__ void bn_finalize_kernel(const float* __restrict__ part, int G, int C, float count,
+// acc[2][C] -> scale/shift (+mean, invstd), running stats update. One thread per channel.
+__global__ void bn_finalize_kernel(float* __restrict__ part, int G, int C, float count,
                                    const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
                                    float momentum, float* __restrict__ run_mean, float* __restrict__ run_var,
                                    float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ mean_out,
                                    float* __restrict__ invstd_out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int g = 0; g < G; ++g) {
-    s += part[((size_t)g * 2 + 0) * C + c];
-    q += part[((size_t)g * 2 + 1) * C + c];
-  }
+  float* acc = part;
+  const double s = acc[c], q = acc[C + c];
+  acc[c] = 0.f;
+  acc[C + c] = 0.f;
   const double mean = s / count;
   double var = q / count - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -188,24 +190,23 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(DySrc src, const bf1
     const int cvv = ch / 8, j = ch % 8;
     float acc = 0.f;
     for (int r = 0; r < rpp; ++r) acc += red[(r * CV + cvv) * 16 + which * 8 + j];
-    part[((size_t)blockIdx.x * 2 + which) * C + ch] = acc;
+    atomicAdd(part + (size_t)which * C + ch, acc);
   }
 }
 
-// part[G][2][C] (sum g, sum g*xhat) -> dbeta, dgamma (written to the gradient buffer, scaled by
+// acc[2][C] (sum g, sum g*xhat; re-zeroed) -> dbeta, dgamma (written to the gradient buffer, scaled by
 // grad_scale and ACCUMULATED if accumulate) + apply coefficients coef[3][C]:
 //   dx = k1 * (g - k2 - xhat * k3),  k1 = gamma*invstd, k2 = sum g / M, k3 = sum g*xhat / M
-__global__ void bn_finalize_bwd_kernel(const float* __restrict__ part, int G, int C, float count,
+__global__ void bn_finalize_bwd_kernel(float* __restrict__ part, int G, int C, float count,
                                        const float* __restrict__ gamma, const float* __restrict__ invstd,
                                        float* __restrict__ dgamma, float* __restrict__ dbeta,
                                        float* __restrict__ coef) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  double s = 0.0, sx = 0.0;
-  for (int g = 0; g < G; ++g) {
-    s += part[((size_t)g * 2 + 0) * C + c];
-    sx += part[((size_t)g * 2 + 1) * C + c];
-  }
+  float* acc = part;
+  const double s = acc[c], sx = acc[C + c];
+  acc[c] = 0.f;
+  acc[C + c] = 0.f;
   dbeta[c] = (float)s;
   dgamma[c] = (float)sx;
   coef[c] = gamma[c] * invstd[c];
@@ -261,7 +262,7 @@ DRN_API int drn_bn_stats(const void* x, float* part, int M, int C, int rows_per_
   return (int)hipGetLastError();
 }
 
-DRN_API int drn_bn_finalize(const float* part, int G, int C, float count, const float* gamma, const float* beta,
+DRN_API int drn_bn_finalize(float* part, int G, int C, float count, const float* gamma, const float* beta,
                             float eps, float momentum, float* run_mean, float* run_var, float* scale, float* shift,
                             float* mean, float* invstd, hipStream_t s) {
   hipLaunchKernelGGL(drn::bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, G, C, count, gamma, beta,
@@ -297,7 +298,7 @@ DRN_API int drn_bn_bwd_reduce(const void* dy, const float* dpool, int pool_hw, c
   return (int)hipGetLastError();
 }
 
-DRN_API int drn_bn_finalize_bwd(const float* part, int G, int C, float count, const float* gamma,
+DRN_API int drn_bn_finalize_bwd(float* part, int G, int C, float count, const float* gamma,
                                 const float* invstd, float* dgamma, float* dbeta, float* coef, hipStream_t s) {
   hipLaunchKernelGGL(drn::bn_finalize_bwd_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, G, C, count, gamma,
                      invstd, dgamma, dbeta, coef);

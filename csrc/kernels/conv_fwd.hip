@@ -7,7 +7,7 @@
 //   k = (r, s, ci) over R*S*C (KRSC weights make k contiguous; NHWC makes ci contiguous).
 // MFMA operand A = weights (rows = output channels), operand B = im2col patches gathered on
 // the fly (cols = output pixels), so each lane's 4 accumulator registers are 4 consecutive
-// output channels of one pixel -> one 8-byte store per accumulator tile.
+// output channels of one pixel (one 16-byte fp32 chunk for the LDS-staged epilogue).
 //
 // Structure: 256 threads = 4 waves; block tile BP pixels x BC channels x BK reduction,
 // register-staged double-buffered LDS (loads for step t+1 in flight while step t computes,
@@ -226,78 +226,77 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(DrnConvFwdArgs a) {
   }
 
   // ---------------- epilogue ----------------
-  const bool want_stats = a.stats != nullptr;
-  float ssum[MI][4], ssq[MI][4];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) ssum[i][r] = ssq[i][r] = 0.f;
-
-  bf16_t* __restrict__ y = reinterpret_cast<bf16_t*>(a.y);
-  const bf16_t* __restrict__ res = reinterpret_cast<const bf16_t*>(a.residual);
+  // The fp32 accumulator tile is staged through LDS ([BP][BC] fp32, 16-byte chunks XOR-swizzled
+  // by row: conflict-free 8-lane ds_write_b128 groups and 16-lane ds_read_b128 groups), then
+  // every lane owns 8 consecutive channels of one pixel: 16-byte residual loads and 16-byte
+  // bf16 stores, whole 2*BC-byte pixel rows per wave instruction (fully coalesced).
+  constexpr int CF = BC / 4;   // fp32 16-byte chunks per staged row
+  constexpr int CHR = BC / 8;  // output 16-byte (8 x bf16) chunks per pixel row
+  constexpr int RPI = 256 / CHR;
+  constexpr int SWM = CF >= 8 ? 7 : CF - 1;  // swizzle mask stays inside a staged row
+  static_assert(BP * BC * 4 <= 2 * STAGE, "epilogue tile must fit the staging LDS");
+  float* tile = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
-    const int c = c0 + wc * WC + i * 16 + 4 * (lane >> 4);
+    const int cf = (wc * WC + i * 16) / 4 + (lane >> 4);  // fp32 chunk of these 4 channels
 #pragma unroll
     for (int j = 0; j < MJ; ++j) {
-      const int m = m0 + wp * WP + j * 16 + (lane & 15);
-      if (m < M && c < a.K) {
-        float v0 = acc[i][j][0], v1 = acc[i][j][1], v2 = acc[i][j][2], v3 = acc[i][j][3];
-        const size_t off = (size_t)m * a.K + c;
-        if (res) {
-          const uint2 rv = *reinterpret_cast<const uint2*>(res + off);
-          v0 += __uint_as_float(rv.x << 16);
-          v1 += __uint_as_float(rv.x & 0xffff0000u);
-          v2 += __uint_as_float(rv.y << 16);
-          v3 += __uint_as_float(rv.y & 0xffff0000u);
-        }
-        uint2 o;
-        o.x = pack2bf(v0, v1);
-        o.y = pack2bf(v2, v3);
-        *reinterpret_cast<uint2*>(y + off) = o;
-        if (want_stats) {
-          const float q0 = __uint_as_float(o.x << 16), q1 = __uint_as_float(o.x & 0xffff0000u);
-          const float q2 = __uint_as_float(o.y << 16), q3 = __uint_as_float(o.y & 0xffff0000u);
-          ssum[i][0] += q0; ssq[i][0] += q0 * q0;
-          ssum[i][1] += q1; ssq[i][1] += q1 * q1;
-          ssum[i][2] += q2; ssq[i][2] += q2 * q2;
-          ssum[i][3] += q3; ssq[i][3] += q3 * q3;
+      const int row = wp * WP + j * 16 + (lane & 15);
+      *reinterpret_cast<f32x4_t*>(tile + row * BC + ((cf ^ (row & SWM)) * 4)) = acc[i][j];
+    }
+  }
+  __syncthreads();
+  const bool want_stats = a.stats != nullptr;
+  bf16_t* __restrict__ y = reinterpret_cast<bf16_t*>(a.y);
+  const bf16_t* __restrict__ res = reinterpret_cast<const bf16_t*>(a.residual);
+  const int ch = tid % CHR;
+  const int c = c0 + ch * 8;
+  float ssum[8], ssq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ssum[j] = ssq[j] = 0.f;
+#pragma unroll
+  for (int it = 0; it < BP / RPI; ++it) {
+    const int row = it * RPI + tid / CHR;
+    const int m = m0 + row;
+    const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(tile + row * BC + (((2 * ch) ^ (row & SWM)) * 4));
+    const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(tile + row * BC + (((2 * ch + 1) ^ (row & SWM)) * 4));
+    if (m < M && c < a.K) {
+      float f[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const size_t off = (size_t)m * a.K + c;
+      if (res) {
+        float r8[8];
+        unpack8(*reinterpret_cast<const uint4*>(res + off), r8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] += r8[j];
+      }
+      const uint4 o = pack8(f);
+      *reinterpret_cast<uint4*>(y + off) = o;
+      if (want_stats) {
+        float q8[8];
+        unpack8(o, q8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ssum[j] += q8[j];
+          ssq[j] += q8[j] * q8[j];
         }
       }
     }
   }
   if (want_stats) {
-    // reduce over the 16 lanes that hold different pixels of the same channels
+    __syncthreads();
+    float* red = tile;  // [256][16]
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          ssum[i][r] += __shfl_xor(ssum[i][r], o, 64);
-          ssq[i][r] += __shfl_xor(ssq[i][r], o, 64);
-        }
-      }
-    // cross-wave combine through LDS: red[wp][BC][2]
-    float* red = reinterpret_cast<float*>(smem);
-    if ((lane & 15) == 0) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int cl = wc * WC + i * 16 + 4 * (lane >> 4) + r;
-          red[(wp * BC + cl) * 2 + 0] = ssum[i][r];
-          red[(wp * BC + cl) * 2 + 1] = ssq[i][r];
-        }
+    for (int j = 0; j < 8; ++j) {
+      red[tid * 16 + j] = ssum[j];
+      red[tid * 16 + 8 + j] = ssq[j];
     }
     __syncthreads();
-    if (tid < BC * 2) {
+    if (tid < 2 * BC) {
       const int cl = tid >> 1, which = tid & 1;
+      const int chh = cl >> 3, j = cl & 7;
       float s = 0.f;
-#pragma unroll
-      for (int w = 0; w < WAVES_P; ++w) s += red[(w * BC + cl) * 2 + which];
-      const int c = c0 + cl;
-      if (c < a.K) a.stats[((size_t)tp * 2 + which) * a.K + c] = s;
+      for (int t2 = chh; t2 < 256; t2 += CHR) s += red[t2 * 16 + which * 8 + j];
+      if (c0 + cl < a.K) atomicAdd(a.stats + (size_t)which * a.K + c0 + cl, s);
     }
   }
 }
@@ -337,7 +336,7 @@ DRN_API int drn_conv_fwd_tiles_p(int M, int K) {
 }
 
 DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s) {
-  if ((a->C % 8) != 0 || (a->K % 4) != 0) return (int)hipErrorInvalidValue;
+  if ((a->C % 8) != 0 || (a->K % 8) != 0) return (int)hipErrorInvalidValue;
   if (a->dil != 1 && a->dil != 2) return (int)hipErrorInvalidValue;
   const bool pro = a->in_scale != nullptr;
   const bool dil2 = a->dil == 2;

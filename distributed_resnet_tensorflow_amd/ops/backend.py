@@ -58,7 +58,18 @@ def tflip_table(descs):
 # ----------------------------------------------------------------------------------------------
 # HIP backend
 # ----------------------------------------------------------------------------------------------
-class HipBackend:
+class _Common:
+    @staticmethod
+    def bn_stats_blocks(M, C):
+        """Rows of a BN statistics accumulator: always 1 ([2][C] accumulated in place)."""
+        return 1
+
+    @staticmethod
+    def conv_stats_tiles(M, K):
+        return 1
+
+
+class HipBackend(_Common):
     name = "hip"
     act_dtype = torch.bfloat16
     acc_dtype = torch.float32
@@ -87,12 +98,8 @@ class HipBackend:
         a.stride, a.pad_h, a.pad_w, a.dil = g.stride, g.pad_h, g.pad_w, g.dil
         a.relu_in = 1 if relu_in else 0
         if stats is not None:
-            need = self.conv_stats_tiles(N * P * Q, K)
-            assert stats.numel() >= need * 2 * K, "stats buffer too small"
+            assert stats.numel() >= 2 * K and stats.dtype == torch.float32, "stats accumulator must be fp32 [2][K]"
         return a
-
-    def conv_stats_tiles(self, M, K):
-        return self.L.drn_conv_fwd_tiles_p(M, K)
 
     def launch_conv(self, a):
         _lib.check(self.L.drn_conv_fwd(ctypes.byref(a), self.stream()), "drn_conv_fwd")
@@ -157,16 +164,13 @@ class HipBackend:
         rpb = max(rpp, ((M + G_target - 1) // G_target + rpp - 1) // rpp * rpp)
         return rpb
 
-    def bn_stats_blocks(self, M, C):
-        rpb = self.bn_rows_per_block(M, C)
-        return (M + rpb - 1) // rpb
-
     def bn_stats(self, x, part):
+        """part[2][C] += (sum, sumsq) over rows of x."""
         C = x.shape[-1]
         M = x.numel() // C
         rpb = self.bn_rows_per_block(M, C)
         _lib.check(self.L.drn_bn_stats(x.data_ptr(), part.data_ptr(), M, C, rpb, self.stream()), "drn_bn_stats")
-        return (M + rpb - 1) // rpb
+        return 1
 
     def bn_finalize(self, part, G, count, gamma, beta, run_mean, run_var, scale, shift, mean, invstd,
                     momentum, eps, update_running=True):
@@ -195,7 +199,7 @@ class HipBackend:
         _lib.check(self.L.drn_bn_bwd_reduce(_ptr(dy), _ptr(dpool), pool_hw, x.data_ptr(), scale.data_ptr(),
                                             shift.data_ptr(), mean.data_ptr(), invstd.data_ptr(), part.data_ptr(),
                                             M, C, rpb, 1 if relu else 0, self.stream()), "drn_bn_bwd_reduce")
-        return (M + rpb - 1) // rpb
+        return 1
 
     def bn_finalize_bwd(self, part, G, count, gamma, invstd, dgamma, dbeta, coef):
         _lib.check(self.L.drn_bn_finalize_bwd(part.data_ptr(), G, gamma.numel(), float(count), gamma.data_ptr(),
@@ -308,7 +312,7 @@ def _dilate(xc, dil):
     return out
 
 
-class RefBackend:
+class RefBackend(_Common):
     name = "ref"
 
     def __init__(self, device="cpu", dtype=torch.float32):
@@ -331,12 +335,8 @@ class RefBackend:
         y.copy_(out)
         if stats is not None:
             yy = y.to(_DT[0]).reshape(-1, K)
-            stats.zero_()
-            stats.view(-1)[:K].copy_(yy.sum(0))
-            stats.view(-1)[K:2 * K].copy_((yy * yy).sum(0))
-
-    def conv_stats_tiles(self, M, K):
-        return 1
+            stats.view(-1)[:K].add_(yy.sum(0))
+            stats.view(-1)[K:2 * K].add_((yy * yy).sum(0))
 
     def wgrad_ws_elems(self, M, K, R, S, C):
         return 0
@@ -348,20 +348,18 @@ class RefBackend:
         dw = torch.nn.grad.conv2d_weight(xc, (K, C, R, S), dy.to(_DT[0]).permute(0, 3, 1, 2), stride=g.stride)
         out.copy_(dw.permute(0, 2, 3, 1))
 
-    def bn_stats_blocks(self, M, C):
-        return 1
-
     def bn_stats(self, x, part):
         C = x.shape[-1]
         xx = x.to(_DT[0]).reshape(-1, C)
-        part.view(-1)[:C].copy_(xx.sum(0))
-        part.view(-1)[C:2 * C].copy_((xx * xx).sum(0))
+        part.view(-1)[:C].add_(xx.sum(0))
+        part.view(-1)[C:2 * C].add_((xx * xx).sum(0))
         return 1
 
     def bn_finalize(self, part, G, count, gamma, beta, run_mean, run_var, scale, shift, mean, invstd,
                     momentum, eps, update_running=True):
         C = gamma.numel()
-        p = part.view(-1)[:G * 2 * C].view(G, 2, C).double().sum(0)
+        p = part.view(-1)[:2 * C].view(2, C).double().clone()
+        part.view(-1)[:2 * C].zero_()
         mu = p[0] / count
         var = (p[1] / count - mu * mu).clamp_min(0)
         istd = 1.0 / torch.sqrt(var + eps)
@@ -400,13 +398,14 @@ class RefBackend:
         if relu:
             d = d * ((xx * scale + shift) > 0).to(_DT[0])
         xh = (xx - mean) * invstd
-        part.view(-1)[:C].copy_(d.sum(0))
-        part.view(-1)[C:2 * C].copy_((d * xh).sum(0))
+        part.view(-1)[:C].add_(d.sum(0))
+        part.view(-1)[C:2 * C].add_((d * xh).sum(0))
         return 1
 
     def bn_finalize_bwd(self, part, G, count, gamma, invstd, dgamma, dbeta, coef):
         C = gamma.numel()
-        p = part.view(-1)[:G * 2 * C].view(G, 2, C).double().sum(0)
+        p = part.view(-1)[:2 * C].view(2, C).double().clone()
+        part.view(-1)[:2 * C].zero_()
         dbeta.copy_(p[0].to(_DT[0]))
         dgamma.copy_(p[1].to(_DT[0]))
         coef.view(3, C)[0].copy_(gamma * invstd)

@@ -122,8 +122,7 @@ class Executor:
         return op, wt_off
 
     def _stats_for(self, M: int, C: int) -> tuple[torch.Tensor, int]:
-        G = self.be.conv_stats_tiles(M, C)
-        return self._f32(G, 2, C), G
+        return self._f32(2, C), 1
 
     def _alloc(self):
         sp, N = self.spec, self.N
@@ -141,8 +140,7 @@ class Executor:
             ph = sp.pool_hw
             self.pool_out = self._act(N, ph, ph, sp.stem.cout)
             self.pool_arg = torch.zeros(N, ph, ph, sp.stem.cout, dtype=torch.uint8, device=self.device)
-            Gp = be.bn_stats_blocks(N * ph * ph, sp.stem.cout)
-            self.pool_stats, self.pool_G = self._f32(Gp, 2, sp.stem.cout), Gp
+            self.pool_stats, self.pool_G = self._f32(2, sp.stem.cout), 1
             x, x_stats, x_G = self.pool_out, self.pool_stats, self.pool_G
             self.stem_stats, self.stem_G = None, 0
         else:
@@ -213,11 +211,7 @@ class Executor:
         self.g_a = self._act(max_act)
         self.g_b = self._act(max_act)
         self.g_c = self._act(max_act)
-        part = 0
-        for b in [bb for bp in self.blocks for bb in bp.bn] + [self.final_bn]:
-            M = b.rows
-            part = max(part, be.bn_stats_blocks(M, b.bn.c) * 2 * b.bn.c)
-        self.bn_part = self._f32(max(part, 16))
+        self.bn_part = self._f32(2 * max(b.bn.c for bp in self.blocks for b in bp.bn + [self.final_bn]))
         self.bn_coef = self._f32(3 * max(b.bn.c for bp in self.blocks for b in bp.bn + [self.final_bn]))
         self.wgrad_ws = self._f32(max(ws_need, 16))
         # data-gradient weights (flipped / channel-transposed), one flat buffer + device table
