@@ -1,0 +1,281 @@
+"""ImageNet TFRecord input pipeline + VGG preprocessing.
+
+Reference: resnet_imagenet_main.py:103-183 (filenames / record_parser / input_fn) and
+vgg_preprocessing.py:229-363.
+  * shards <dir>/train-%05d-of-01024 and <dir>/validation-%05d-of-00128 (falls back to any
+    `train-*` / `validation-*` files present);
+  * tf.Example: 'image/encoded' (JPEG/PNG bytes), 'image/class/label' (int64, 1..1000 with
+    0 = background -> 1001 classes); bounding boxes are parsed-and-ignored in the reference too;
+  * train: file-order shuffle, example shuffle buffer 1500, smaller side resized to U{256..512}
+    (aspect preserving, TF1 legacy bilinear), random 224 crop, random flip, RGB mean
+    subtraction of (123.68, 116.78, 103.94)/255 on [0,1] pixels; eval: smaller side 256,
+    central 224 crop, mean subtraction.
+Host side: TFRecord scan (native CRC check), Example parsing, JPEG decode (PIL, thread pool)
+and the per-image geometry draws. GPU side: one fused resize+crop+flip+mean-sub kernel over
+the packed decoded batch (csrc/kernels/augment.hip, drn_vgg_preprocess); the CPU path runs the
+same math in numpy (RefBackend.vgg_preprocess).
+"""
+from __future__ import annotations
+
+import glob
+import io
+import os
+import queue
+import threading
+from concurrent.futures import ThreadPoolExecutor
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+from ..utils import pbwire as pb
+from ..utils.tfrecord import TFRecordWriter, read_records
+
+IMAGE_SIZE = 224
+NUM_CLASSES = 1001
+NUM_IMAGES = {"train": 1281167, "validation": 50000}
+FILE_SHUFFLE_BUFFER = 1024
+SHUFFLE_BUFFER = 1500
+RGB_MEANS = (123.68 / 255, 116.78 / 255, 103.94 / 255)
+RESIZE_MIN, RESIZE_MAX = 256, 512
+
+# numpy mirror of csrc/kernels/augment.hip `struct ImgDesc`
+IMG_DESC = np.dtype([("offset", "<i8"), ("H", "<i4"), ("W", "<i4"), ("rh", "<i4"), ("rw", "<i4"),
+                     ("cy", "<i4"), ("cx", "<i4"), ("flip", "<i4"), ("pad", "<i4")])
+
+
+def filenames(is_training: bool, data_dir: str) -> List[str]:
+    if is_training:
+        names = [os.path.join(data_dir, "train-%05d-of-01024" % i) for i in range(1024)]
+    else:
+        names = [os.path.join(data_dir, "validation-%05d-of-00128" % i) for i in range(128)]
+    if all(os.path.exists(n) for n in names):
+        return names
+    pat = "train-*" if is_training else "validation-*"
+    found = sorted(glob.glob(os.path.join(data_dir, pat)))
+    if found:
+        return found
+    raise FileNotFoundError(f"no ImageNet {'train' if is_training else 'validation'} shards in {data_dir}")
+
+
+# -- tf.Example ------------------------------------------------------------------------------
+# Example { Features features = 1 }  Features { map<string, Feature> feature = 1 }
+# Feature { BytesList bytes_list = 1; FloatList float_list = 2; Int64List int64_list = 3 }
+def parse_example(buf: bytes) -> dict:
+    out = {}
+    ex = pb.decode(buf)
+    for feats in ex.get(1, []):
+        for entry in pb.decode(feats).get(1, []):
+            e = pb.decode(entry)
+            key = e[1][0].decode() if 1 in e else ""
+            if 2 not in e:
+                continue
+            f = pb.decode(e[2][0])
+            if 1 in f:
+                out[key] = [bytes(v) for v in pb.decode(f[1][0]).get(1, [])]
+            elif 3 in f:
+                il = pb.decode(f[3][0]).get(1, [])
+                vals = []
+                for v in il:
+                    if isinstance(v, (bytes, bytearray, memoryview)):  # packed
+                        pos, b = 0, bytes(v)
+                        while pos < len(b):
+                            x, pos = pb.read_varint(b, pos)
+                            vals.append(pb.signed64(x))
+                    else:
+                        vals.append(pb.signed64(v))
+                out[key] = vals
+            elif 2 in f:
+                fl = pb.decode(f[2][0]).get(1, [])
+                vals = []
+                for v in fl:
+                    b = bytes(v)
+                    vals.extend(np.frombuffer(b, dtype="<f4").tolist())
+                out[key] = vals
+    return out
+
+
+def make_example(image_bytes: bytes, label: int, fmt: str = "jpeg") -> bytes:
+    def feat_bytes(b):
+        return pb.f_bytes(1, pb.f_bytes(1, b))
+
+    def feat_int(v):
+        return pb.f_bytes(3, pb.f_bytes(1, pb.varint(v)))
+
+    def entry(k, f):
+        return pb.f_bytes(1, pb.f_string(1, k) + pb.f_bytes(2, f))
+
+    feats = entry("image/encoded", feat_bytes(image_bytes)) + entry("image/format", feat_bytes(fmt.encode())) + \
+        entry("image/class/label", feat_int(label))
+    return pb.f_bytes(1, feats)
+
+
+def decode_image(b: bytes) -> np.ndarray:
+    from PIL import Image
+    with Image.open(io.BytesIO(b)) as im:
+        return np.asarray(im.convert("RGB"), dtype=np.uint8)
+
+
+# -- VGG geometry ------------------------------------------------------------------------------
+def smallest_size_at_least(h: int, w: int, side: int) -> Tuple[int, int]:
+    scale = side / w if h > w else side / h
+    return int(h * scale), int(w * scale)
+
+
+def draw_geometry(h: int, w: int, is_training: bool, rng: np.random.Generator, out: int = IMAGE_SIZE):
+    side = int(rng.integers(RESIZE_MIN, RESIZE_MAX + 1)) if is_training else RESIZE_MIN
+    rh, rw = smallest_size_at_least(h, w, side)
+    if is_training:
+        cy = int(rng.integers(0, rh - out + 1))
+        cx = int(rng.integers(0, rw - out + 1))
+        flip = int(rng.integers(0, 2))
+    else:
+        cy, cx, flip = (rh - out) // 2, (rw - out) // 2, 0
+    return rh, rw, cy, cx, flip
+
+
+def vgg_preprocess_np(img: np.ndarray, rh: int, rw: int, cy: int, cx: int, flip: int, out: int = IMAGE_SIZE):
+    """CPU reference of the fused GPU kernel: legacy TF bilinear (src = dst*in/out), crop, flip,
+    /255, mean subtraction. Returns float32 [out,out,3]."""
+    H, W = img.shape[:2]
+    ys = (np.arange(out) + cy) * (H / rh)
+    xs_idx = np.arange(out)
+    if flip:
+        xs_idx = out - 1 - xs_idx
+    xs = (xs_idx + cx) * (W / rw)
+    y0 = np.clip(np.floor(ys).astype(np.int64), 0, H - 1)
+    x0 = np.clip(np.floor(xs).astype(np.int64), 0, W - 1)
+    y1 = np.minimum(y0 + 1, H - 1)
+    x1 = np.minimum(x0 + 1, W - 1)
+    wy = (ys - y0)[:, None, None].astype(np.float32)
+    wx = (xs - x0)[None, :, None].astype(np.float32)
+    f = img.astype(np.float32)
+    a, b = f[y0][:, x0], f[y0][:, x1]
+    c, d = f[y1][:, x0], f[y1][:, x1]
+    top = a + (b - a) * wx
+    bot = c + (d - c) * wx
+    res = (top + (bot - top) * wy) / 255.0
+    return res - np.array(RGB_MEANS, dtype=np.float32)
+
+
+class ImagenetLoader:
+    """Background pipeline producing packed decoded batches:
+    (packed uint8 buffer, IMG_DESC array [B], int32 labels [B])."""
+
+    def __init__(self, data_dir: str, batch_size: int, is_training: bool, seed: int = 0, rank: int = 0,
+                 world: int = 1, num_threads: int = 8, prefetch: int = 3, num_epochs: Optional[int] = None):
+        self.files = filenames(is_training, data_dir)
+        if is_training and world > 1:
+            self.files = self.files[rank::world] or self.files
+        self.bs, self.train, self.seed, self.rank = batch_size, is_training, seed, rank
+        self.num_epochs = num_epochs
+        self.pool = ThreadPoolExecutor(max_workers=max(1, num_threads))
+        self.q: "queue.Queue" = queue.Queue(maxsize=max(1, prefetch))
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+        self._t.start()
+
+    def _records(self):
+        rng = np.random.default_rng([self.seed, self.rank, 17])
+        epoch = 0
+        while not self._stop.is_set():
+            if self.num_epochs is not None and epoch >= self.num_epochs:
+                return
+            files = list(self.files)
+            if self.train:
+                rng.shuffle(files)
+            buf = []
+            for fn in files:
+                for rec in read_records(fn):
+                    if self.train:
+                        buf.append(rec)
+                        if len(buf) >= SHUFFLE_BUFFER:
+                            j = int(rng.integers(0, len(buf)))
+                            buf[j], buf[-1] = buf[-1], buf[j]
+                            yield buf.pop()
+                    else:
+                        yield rec
+            while buf:
+                j = int(rng.integers(0, len(buf)))
+                buf[j], buf[-1] = buf[-1], buf[j]
+                yield buf.pop()
+            epoch += 1
+
+    @staticmethod
+    def _decode(rec: bytes):
+        ex = parse_example(rec)
+        img = decode_image(ex["image/encoded"][0])
+        label = int(ex.get("image/class/label", [-1])[0])
+        return img, label
+
+    def _run(self):
+        rng = np.random.default_rng([self.seed, self.rank, 99])
+        batch = []
+        try:
+            for rec in self._records():
+                batch.append(rec)
+                if len(batch) < self.bs:
+                    continue
+                decoded = list(self.pool.map(self._decode, batch))
+                batch = []
+                sizes = [d[0].size for d in decoded]
+                packed = np.empty(sum(sizes), dtype=np.uint8)
+                desc = np.zeros(self.bs, dtype=IMG_DESC)
+                labels = np.empty(self.bs, dtype=np.int32)
+                off = 0
+                for i, (img, lab) in enumerate(decoded):
+                    h, w = img.shape[:2]
+                    packed[off:off + img.size] = img.reshape(-1)
+                    rh, rw, cy, cx, flip = draw_geometry(h, w, self.train, rng)
+                    desc[i] = (off, h, w, rh, rw, cy, cx, flip, 0)
+                    labels[i] = lab
+                    off += img.size
+                while not self._stop.is_set():
+                    try:
+                        self.q.put((packed, desc, labels), timeout=0.1)
+                        break
+                    except queue.Full:
+                        continue
+                if self._stop.is_set():
+                    return
+        finally:
+            self.q.put(None)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        item = self.q.get()
+        if item is None:
+            raise StopIteration
+        return item
+
+    def close(self):
+        self._stop.set()
+        try:
+            while True:
+                self.q.get_nowait()
+        except queue.Empty:
+            pass
+        self._t.join(timeout=2)
+        self.pool.shutdown(wait=False)
+
+
+def write_fake_imagenet(dirpath: str, shards: int = 2, per_shard: int = 8, is_training: bool = True,
+                        seed: int = 0, num_classes: int = 1001) -> List[str]:
+    """Writes small ImageNet-format TFRecord shards with random JPEGs (tests, smoke runs)."""
+    from PIL import Image
+    os.makedirs(dirpath, exist_ok=True)
+    rng = np.random.default_rng(seed)
+    out = []
+    for s in range(shards):
+        name = ("train-%05d-of-01024" if is_training else "validation-%05d-of-00128") % s
+        path = os.path.join(dirpath, name)
+        with TFRecordWriter(path) as w:
+            for _ in range(per_shard):
+                h, wd = int(rng.integers(200, 330)), int(rng.integers(200, 330))
+                arr = rng.integers(0, 256, (h, wd, 3), dtype=np.uint8)
+                b = io.BytesIO()
+                Image.fromarray(arr).save(b, format="JPEG", quality=90)
+                w.write(make_example(b.getvalue(), int(rng.integers(1, num_classes))))
+        out.append(path)
+    return out

@@ -20,6 +20,7 @@ from __future__ import annotations
 import ctypes
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -531,6 +532,19 @@ class RefBackend(_Common):
             std = crop.std(unbiased=False)
             adj = torch.maximum(std, torch.tensor(1.0 / (crop.numel() ** 0.5)))
             res[n, :, :, :3] = ((crop - mean) / adj).permute(1, 2, 0)
+        out.copy_(res)
+
+    def vgg_preprocess(self, packed_u8, desc, out, means):
+        from ..data.imagenet import vgg_preprocess_np
+        N, OH, OW, _ = out.shape
+        d = desc if isinstance(desc, np.ndarray) else desc.cpu().numpy()
+        buf = packed_u8.cpu().numpy() if hasattr(packed_u8, "cpu") else packed_u8
+        res = torch.zeros(N, OH, OW, out.shape[-1], dtype=_DT[0])
+        for i in range(N):
+            r = d[i]
+            img = buf[int(r["offset"]):int(r["offset"]) + int(r["H"]) * int(r["W"]) * 3].reshape(int(r["H"]), int(r["W"]), 3)
+            res[i, :, :, :3] = torch.from_numpy(vgg_preprocess_np(img, int(r["rh"]), int(r["rw"]), int(r["cy"]),
+                                                                  int(r["cx"]), int(r["flip"]), OH))
         out.copy_(res)
 
     def synthetic_images(self, out, seed):

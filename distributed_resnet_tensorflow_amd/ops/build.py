@@ -26,6 +26,8 @@ KERNELS = CSRC / "kernels"
 INCLUDE = CSRC / "include"
 LIB_DIR = Path(__file__).resolve().parent
 LIB_PATH = LIB_DIR / "libdrn_kernels.so"
+HOST_LIB_PATH = LIB_DIR / "libdrn_host.so"
+HOST_SRC = CSRC / "host"
 OBJ_DIR = REPO / "build" / "obj"
 ARCH = os.environ.get("DRN_OFFLOAD_ARCH", "gfx950")
 
@@ -58,8 +60,27 @@ def _compile(src: Path, extra: list[str]) -> Path:
     return obj
 
 
+def build_host(force: bool = False, verbose: bool = True) -> Path:
+    """Compile the native host helpers (CRC32C, TFRecord scan, CIFAR gather) with g++."""
+    srcs = sorted(HOST_SRC.glob("*.cc"))
+    newest = max(s.stat().st_mtime for s in srcs)
+    if HOST_LIB_PATH.exists() and HOST_LIB_PATH.stat().st_mtime >= newest and not force:
+        return HOST_LIB_PATH
+    cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
+    tmp = HOST_LIB_PATH.with_suffix(".so.tmp")
+    cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-o", str(tmp)] + [str(s) for s in srcs]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"host library build failed:\n{res.stderr[-4000:]}")
+    os.replace(tmp, HOST_LIB_PATH)
+    if verbose:
+        print(f"[drn.build] built {HOST_LIB_PATH}")
+    return HOST_LIB_PATH
+
+
 def build(force: bool = False, verbose: bool = True, extra: list[str] | None = None) -> Path:
     """Compile all kernels for gfx950 and link libdrn_kernels.so (incremental)."""
+    build_host(force=force, verbose=verbose)
     OBJ_DIR.mkdir(parents=True, exist_ok=True)
     srcs = sources()
     if force:

@@ -379,9 +379,10 @@ class Executor:
     def set_lr(self, lr: float):
         self.lr_t.fill_(float(lr))
 
-    def apply_gradients(self, grad_scale: float = 1.0):
+    def apply_gradients(self, grad_scale: float = 1.0, grad: Optional[torch.Tensor] = None):
         P = self.P
-        self.be.sgd_momentum(P.master, P.momentum, P.grad, P.wbf16, self.lr_t, self.mom, self.wd, grad_scale)
+        g = P.grad if grad is None else grad
+        self.be.sgd_momentum(P.master, P.momentum, g, P.wbf16, self.lr_t, self.mom, self.wd, grad_scale)
         if self.wt_n:
             src = P.wbf16 if P.wbf16 is not None else P.master
             table = self.wt_table if self.is_hip else self.wt_table.cpu()

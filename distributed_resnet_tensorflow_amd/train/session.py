@@ -1,0 +1,139 @@
+"""Training session: the MonitoredTrainingSession analog (reference resnet_cifar_main.py:309-337).
+
+restore-or-init from `checkpoint_dir` (chief restores, then a rank-0 broadcast replaces both
+the PS variable fetch and Horovod's BroadcastGlobalVariablesHook), chief-only hooks (summaries,
+checkpoints), per-step LR feed, `should_stop()` via hooks, and a final checkpoint on exit.
+One step = feeder.next() -> [HIP graph replay | eager fwd/bwd (+ bucketed all-reduce
+overlapped with backward) + fused SGD].
+"""
+from __future__ import annotations
+
+import logging
+import time
+from typing import Callable, List, Optional
+
+import torch
+
+from ..ckpt.saver import Saver, latest_checkpoint
+from ..ops.backend import HipBackend, RefBackend
+from ..parallel.engine import DataParallelEngine
+from ..runtime.executor import Executor
+from ..runtime.graph import StepGraph
+from ..runtime.state import export_state, import_state
+from .hooks import Hook
+
+log = logging.getLogger("drn")
+
+
+def make_backend(device: str):
+    if str(device).startswith("cuda"):
+        return HipBackend(device)
+    return RefBackend("cpu")
+
+
+class TrainingSession:
+    def __init__(self, spec, batch: int, cluster, *, weight_decay: float, lr_schedule, checkpoint_dir: str = "",
+                 max_to_keep: int = 5, seed: int = 0, use_graph: bool = True, sync_mode: str = "sync",
+                 bucket_mb: float = 25.0, meta: Optional[dict] = None):
+        self.cluster = cluster
+        self.spec = spec
+        self.device = torch.device(cluster.device)
+        self.be = make_backend(cluster.device)
+        self.ex = Executor(spec, batch, self.be, self.device, seed=seed, weight_decay=weight_decay)
+        self.lr = lr_schedule
+        self.meta = meta or {}
+        self.engine = DataParallelEngine(self.ex, bucket_mb=bucket_mb, mode=sync_mode) if cluster.distributed else None
+        self.world = cluster.world
+        self.ckpt_dir = checkpoint_dir
+        self.saver = Saver(checkpoint_dir, max_to_keep) if (checkpoint_dir and cluster.is_chief) else None
+        self.data_state = {}
+        self.restored_from = None
+        self._restore()
+        self.use_graph = use_graph and self.device.type == "cuda" and not cluster.distributed
+        self._graph: Optional[StepGraph] = None
+        self._metrics_cache = None
+        self.cur_lr = float("nan")
+
+    # -- state -----------------------------------------------------------------------------------
+    @property
+    def global_step(self) -> int:
+        return self.ex.P.global_step
+
+    def _restore(self):
+        prefix = latest_checkpoint(self.ckpt_dir) if self.ckpt_dir else None
+        if prefix is not None and (self.cluster.is_chief or not self.cluster.distributed):
+            tensors = Saver.restore(prefix)
+            self.data_state = import_state(self.ex, tensors)
+            self.restored_from = prefix
+            log.info("Restored %s (global_step %d)", prefix, self.ex.P.global_step)
+        if self.engine is not None:
+            self.engine.broadcast_parameters()
+            if self.cluster.is_chief is False:
+                self.data_state = {}
+
+    def save(self, step: Optional[int] = None, blocking: bool = True):
+        if self.saver is None:
+            return None
+        step = self.global_step if step is None else step
+        extra = dict(self.data_state)
+        tensors = export_state(self.ex, extra)
+        path = self.saver.save(step, tensors, self.meta, blocking=blocking)
+        log.info("Saving checkpoints for %d into %s", step, path)
+        return path
+
+    # -- stepping ----------------------------------------------------------------------------------
+    def _step_body(self):
+        ex = self.ex
+        ex.forward(train=True)
+        if self.engine is not None:
+            self.engine.begin_step()
+            ex.backward()
+            g = self.engine.finish()
+            ex.apply_gradients(grad_scale=1.0 / self.world, grad=g)
+        else:
+            ex.backward()
+            ex.apply_gradients()
+
+    def step(self):
+        """One synchronous training step on the batch already in ex.images / ex.labels."""
+        self.cur_lr = self.lr.lr_for_step()
+        self.ex.set_lr(self.cur_lr)
+        if self.use_graph:
+            if self._graph is None:
+                self._graph = StepGraph(self._step_body, warmup=1)  # warm-up = this real step
+            else:
+                self._graph.replay()
+        else:
+            self._step_body()
+        self.lr.after_step(self.ex.P.global_step)
+        self.ex.P.global_step += 1
+        self._metrics_cache = None
+
+    def metrics(self) -> dict:
+        if self._metrics_cache is None:
+            m = self.ex.metrics()
+            m["learning_rate"] = self.cur_lr
+            self._metrics_cache = m
+        return dict(self._metrics_cache)
+
+    def run(self, feeder, hooks: List[Hook], chief_hooks: List[Hook] = ()):
+        hooks = list(hooks) + (list(chief_hooks) if self.cluster.is_chief else [])
+        for h in hooks:
+            h.begin(self)
+        try:
+            while not any(h.should_stop(self.global_step) for h in hooks):
+                if not feeder.next():
+                    break
+                self.data_state = feeder.state()
+                for h in hooks:
+                    h.before_step(self, self.global_step)
+                self.step()
+                for h in hooks:
+                    h.after_step(self, self.global_step, self.metrics)
+        finally:
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            for h in hooks:
+                h.end(self)
+            if self.saver is not None:
+                self.saver.wait()

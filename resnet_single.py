@@ -1,0 +1,12 @@
+#!/usr/bin/env python3
+"""resnet_single.py — same entry point, flags and behaviour as the reference's resnet_single.py, running on
+the MI355X-native engine (see distributed_resnet_tensorflow_amd/cli.py for the mapping)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from distributed_resnet_tensorflow_amd.cli import single_main  # noqa: E402
+
+if __name__ == "__main__":
+    sys.exit(single_main())

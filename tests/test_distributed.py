@@ -1,0 +1,93 @@
+"""Fake-cluster tests (the analog of the reference's localhost PS/worker runs,
+scripts/submit_mac_dist.sh): gloo backend, world 2 on CPU, one process per rank."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _grads_for(spec, N, shard, seed):
+    from distributed_resnet_tensorflow_amd.ops.backend import RefBackend
+    from distributed_resnet_tensorflow_amd.runtime.executor import Executor
+    ex = Executor(spec, N, RefBackend(), "cpu", seed=seed)
+    g = torch.Generator().manual_seed(100 + shard)
+    ex.images[..., :3] = torch.randn(N, 32, 32, 3, generator=g)
+    ex.labels.copy_(torch.randint(0, 10, (N,), generator=g, dtype=torch.int32))
+    return ex
+
+
+def _worker(rank, world, port, mode, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2
+        from distributed_resnet_tensorflow_amd.parallel.engine import DataParallelEngine
+        spec = cifar_resnet_v2(8)
+        N = 4
+        ex = _grads_for(spec, N, rank, seed=1 + rank)   # different init on purpose: broadcast must fix it
+        eng = DataParallelEngine(ex, bucket_mb=0.05, mode=mode)
+        assert len(eng.buckets) > 1
+        eng.broadcast_parameters()
+        # expected: mean over ranks of each rank's local gradient (per-replica BN, reference semantics)
+        exp = torch.zeros_like(ex.P.grad)
+        for r in range(world):
+            e2 = _grads_for(spec, N, r, seed=1)
+            e2.forward(True)
+            e2.backward()
+            exp += e2.P.grad / world
+        ex.forward(True)
+        eng.begin_step()
+        ex.backward()
+        g = eng.finish()
+        if mode == "sync":
+            err = ((g / world - exp).norm() / exp.norm()).item()
+            w_before = ex.P.master.clone()
+            ex.set_lr(0.1)
+            ex.apply_gradients(grad_scale=1.0 / world, grad=g)
+            out = torch.stack([ex.P.master.sum(), (ex.P.master - w_before).norm()])
+            gathered = [torch.zeros_like(out) for _ in range(world)]
+            dist.all_gather(gathered, out)
+            same = all(torch.allclose(gathered[0], t) for t in gathered)
+            q.put((rank, err, same))
+        else:
+            # delayed mode: first step applies nothing, second step applies step-1's average
+            assert float(g.abs().sum()) == 0.0
+            ex.forward(True)
+            eng.begin_step()
+            ex.backward()
+            g2 = eng.finish()
+            err = ((g2 / world - exp).norm() / exp.norm()).item()
+            q.put((rank, err, True))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), False))
+
+
+@pytest.mark.parametrize("mode", ["sync", "delayed"])
+def test_allreduce_dp_equals_mean_of_replica_gradients(mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, err, same in res:
+        assert isinstance(err, float), err
+        assert err < 1e-5, (rank, err)
+        assert same
