@@ -7,17 +7,25 @@
 // Both operands are stored with the NON-reduction dim contiguous (NHWC rows), so the
 // fragments are read out of LDS with the gfx950 hardware transpose `ds_read_b64_tr_b16`
 // (4 rows x 16 cols per 16-lane group, delivered column-major). MFMA operand A = patches
-// (rows = k), operand B = dY (cols = cout): the accumulator then holds 4 consecutive k of
-// one output channel per lane -> 16-byte fp32 stores into the KRSC gradient.
+// (rows = k), operand B = dY (cols = cout): the accumulator holds 4 consecutive k of one output
+// channel per lane -> 16-byte fp32 stores into the KRSC gradient.
 //
-// Block = 4 waves over a 64(k) x BC(cout) tile; each step stages 128 output pixels, every
-// wave owning a 32-pixel MFMA k-slice (intra-block split-K), summed through LDS at the end.
-// Grid z-splits the pixel range (split-K) into fp32 partial slabs reduced deterministically
-// by drn_splitk_reduce (no float atomics: bitwise-reproducible gradients).
-// LDS rows are 128 B with a 16-B chunk XOR swizzle f(row) that makes the transposed reads
-// conflict-free (simulated against the tr_b16 bank rule) and keeps 128-B ds_write groups.
+// Block = 4 waves in a 2x2 arrangement over a BKK(k) x BCO(cout) output tile (each wave
+// BKK/2 x BCO/2); every step stages 64 output pixels (two 32-deep MFMA k-slices) of both
+// operands, register-staged and double-buffered, one barrier per step. The thread->vector
+// assignment keeps each thread on ONE 8-channel chunk of k for the whole kernel (r,s,ci decoded
+// once; the pixel decode per vector uses magic-number division).
+// LDS rows are BKK*2 / BCO*2 bytes with a 32-byte-slot XOR swizzle h(row) chosen so that the
+// 8 rows a 32-lane half reads per transposed read hit 8 distinct bank slots (conflict-free) and
+// every 8-lane ds_write_b128 group stays inside one 128-byte bank window.
+// Grid y splits the pixel range (split-K) into fp32 partial slabs reduced deterministically by
+// drn_splitk_reduce (no float atomics: bitwise-reproducible weight gradients).
 #include "drn_common.h"
 #include "drn_conv.h"
+
+#ifndef DRN_WGRAD_STAGES
+#define DRN_WGRAD_STAGES 2
+#endif
 
 namespace drn {
 
@@ -25,7 +33,18 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const DrnFastDiv& f) {
   return (__umulhi(n, f.m) + n) >> f.s;
 }
 
-__device__ __forceinline__ int swz(int row) { return (((row >> 1) & 1) << 1) | (((row >> 3) & 1) << 2); }
+// 32-byte-slot swizzle for rows of W bytes (W = 128 or 256)
+template <int W>
+__device__ __forceinline__ int slot_swz(int row) {
+  if constexpr (W == 256) return (row & 3) | (((row >> 3) & 1) << 2);
+  return ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
+}
+
+// byte offset of element column `col` (bf16) of `row` in a swizzled image with W-byte rows
+template <int W>
+__device__ __forceinline__ int swz_off(int row, int col) {
+  return row * W + ((((col >> 4) ^ slot_swz<W>(row))) << 5) + (col & 15) * 2;
+}
 
 typedef short s16x4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4v lds_s16x4;
@@ -34,16 +53,19 @@ __device__ __forceinline__ s16x4v tr_read(const char* base, int byte_off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + byte_off));
 }
 
-template <int BC, bool PRO>
-__global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(DrnConvWgradArgs a) {
-  constexpr int BKK = 64;          // k (r,s,ci) columns per block
-  constexpr int BM = 128;          // pixels per step
-  constexpr int TILE = BM * 128;   // bytes per operand image (128-B rows)
-  constexpr int STAGE = 2 * TILE;
-  constexpr int CHD = BC / 8;      // dY chunks per row
-  constexpr int ND = (BM * CHD) / 256;
-  constexpr int MJ = BC / 16;      // cout subtiles
-  static_assert(ND >= 1, "dY tile must cover 256 threads");
+template <int BKK, int BCO, bool PRO, int NST>
+__global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_wgrad_kernel(DrnConvWgradArgs a) {
+  constexpr int BP = 64;                 // pixels per step
+  constexpr int WA = BKK * 2;            // patch image row bytes
+  constexpr int WB = BCO * 2;            // dY image row bytes
+  constexpr int A_BYTES = BP * WA;
+  constexpr int STAGE = A_BYTES + BP * WB;
+  constexpr int CHA = BKK / 8, CHB = BCO / 8;          // 16-byte chunks per row
+  constexpr int NVA = BP * CHA / 256, NVB = BP * CHB / 256;
+  constexpr int RPA = 64 / CHA, RPB = 64 / CHB;        // rows per wave-instruction group
+  constexpr int WKK = BKK / 2, WCO = BCO / 2;          // wave tile
+  constexpr int MI = WKK / 16, MJ = WCO / 16;
+  static_assert(NVA >= 1 && NVB >= 1, "tiles must cover 256 threads");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -51,16 +73,16 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(DrnConvWgradArgs a) 
   const int Ktot = a.R * a.S * a.C;
   const int M = a.N * a.P * a.Q;
   const int nkt = (Ktot + BKK - 1) / BKK;
-  const int bid = blockIdx.x;
-  const int kt = bid % nkt;
-  const int ct = bid / nkt;
-  const int k0 = kt * BKK, c0 = ct * BC;
+  const int kt = blockIdx.x % nkt;
+  const int ct = blockIdx.x / nkt;
+  const int k0 = kt * BKK, c0 = ct * BCO;
   const int split = blockIdx.y;
   const int mbeg = split * a.pix_per_split;
   const int mend = min(M, mbeg + a.pix_per_split);
 
-  // patch loader: lane -> (chunk = lane&7, row = lane>>3 + 8*(wave+4i)), 4 vectors/thread
-  const int pchunk = lane & 7;
+  // patch loader: fixed chunk per thread
+  const int pchunk = lane % CHA;
+  const int prow0 = lane / CHA;
   const int kk = k0 + pchunk * 8;
   const bool kvalid = kk < Ktot;
   int ci = 0, rr = 0, ss = 0;
@@ -78,21 +100,22 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(DrnConvWgradArgs a) 
       sh[j] = kvalid ? a.in_shift[ci + j] : 0.f;
     }
   }
-  // dY loader: lane -> (chunk = lane % CHD, row = lane / CHD + (64/CHD)*(wave+4i))
-  const int dchunk = lane % CHD;
+  const int dchunk = lane % CHB;
+  const int drow0 = lane / CHB;
   const int dc = c0 + dchunk * 8;
   const bool dvalid_c = dc < a.K;
+  const uint32_t PQ = (uint32_t)(a.P * a.Q);
 
-  uint4 rp[4], rd[ND];
+  uint4 rp[NVA], rd[NVB];
   auto load_stage = [&](int mstep) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (lane >> 3) + 8 * (wave + 4 * i);
+    for (int i = 0; i < NVA; ++i) {
+      const int row = prow0 + RPA * (wave + 4 * i);
       const int m = mstep + row;
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
       if (kvalid && m < mend) {
         const uint32_t n = fdiv((uint32_t)m, a.fd_pq);
-        const uint32_t rem = (uint32_t)m - n * (uint32_t)(a.P * a.Q);
+        const uint32_t rem = (uint32_t)m - n * PQ;
         const uint32_t p = fdiv(rem, a.fd_q);
         const uint32_t q = rem - p * (uint32_t)a.Q;
         const int h = (int)p * a.stride - a.pad_h + rr;
@@ -115,8 +138,8 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(DrnConvWgradArgs a) 
       rp[i] = v;
     }
 #pragma unroll
-    for (int i = 0; i < ND; ++i) {
-      const int row = lane / CHD + (64 / CHD) * (wave + 4 * i);
+    for (int i = 0; i < NVB; ++i) {
+      const int row = drow0 + RPB * (wave + 4 * i);
       const int m = mstep + row;
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
       if (dvalid_c && m < mend)
@@ -126,117 +149,113 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(DrnConvWgradArgs a) 
   };
   auto store_stage = [&](char* st) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (lane >> 3) + 8 * (wave + 4 * i);
-      *reinterpret_cast<uint4*>(st + row * 128 + ((pchunk ^ swz(row)) & 7) * 16) = rp[i];
+    for (int i = 0; i < NVA; ++i) {
+      const int row = prow0 + RPA * (wave + 4 * i);
+      *reinterpret_cast<uint4*>(st + swz_off<WA>(row, pchunk * 8)) = rp[i];
     }
-    char* sd = st + TILE;
+    char* sd = st + A_BYTES;
 #pragma unroll
-    for (int i = 0; i < ND; ++i) {
-      const int row = lane / CHD + (64 / CHD) * (wave + 4 * i);
-      *reinterpret_cast<uint4*>(sd + row * 128 + ((dchunk ^ swz(row)) & 7) * 16) = rd[i];
+    for (int i = 0; i < NVB; ++i) {
+      const int row = drow0 + RPB * (wave + 4 * i);
+      *reinterpret_cast<uint4*>(sd + swz_off<WB>(row, dchunk * 8)) = rd[i];
     }
   };
 
-  f32x4_t acc[4][MJ];
+  f32x4_t acc[MI][MJ];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < MJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  const int T = (mend > mbeg) ? (mend - mbeg + BM - 1) / BM : 0;
-  // per-lane transposed-read geometry: group g = lane>>4 owns k-rows 8g..8g+7 of the wave slice
+  const int T = (mend > mbeg) ? (mend - mbeg + BP - 1) / BP : 0;
   const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  const int wk = wave & 1, wc = wave >> 1;
 
   if (T > 0) {
     load_stage(mbeg);
-    store_stage(smem);
-    __syncthreads();
+    if constexpr (NST == 2) {
+      store_stage(smem);
+      __syncthreads();
+    }
   }
   for (int t = 0; t < T; ++t) {
-    const char* cur = smem + (t & 1) * STAGE;
+    const char* cur = smem + (NST == 2 ? (t & 1) * STAGE : 0);
     const bool more = (t + 1) < T;
-    if (more) load_stage(mbeg + (t + 1) * BM);
-    bf16x8_t af[4], bfr[MJ];
-    {
-      s16x4v alo[4], ahi[4], blo[MJ], bhi[MJ];
+    if constexpr (NST == 1) {
+      // single LDS stage (half the LDS -> 2x the resident workgroups): write the registers
+      // loaded during the previous step, then immediately issue the next step's loads
+      store_stage(smem);
+      __syncthreads();
+    }
+    if (more) load_stage(mbeg + (t + 1) * BP);
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int row = 32 * wave + 8 * g + 4 * hh + q4;
-        const int rbase = row * 128;
-        const int sw = swz(row);
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8_t af[MI], bfr[MJ];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int col = 16 * i + 4 * p4;
-          const int off = rbase + (((col >> 3) ^ sw) & 7) * 16 + (col & 7) * 2;
-          if (hh == 0) alo[i] = tr_read(cur, off); else ahi[i] = tr_read(cur, off);
-        }
-#pragma unroll
-        for (int j = 0; j < MJ; ++j) {
-          const int col = 16 * j + 4 * p4;
-          const int off = TILE + rbase + (((col >> 3) ^ sw) & 7) * 16 + (col & 7) * 2;
-          if (hh == 0) blo[j] = tr_read(cur, off); else bhi[j] = tr_read(cur, off);
-        }
+      for (int i = 0; i < MI; ++i) {
+        const int col = wk * WKK + 16 * i + 4 * p4;
+        const int r0 = 32 * ks + 8 * g + q4;
+        const s16x4v lo = tr_read(cur, swz_off<WA>(r0, col));
+        const s16x4v hi = tr_read(cur, swz_off<WA>(r0 + 4, col));
+        af[i] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        af[i] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(alo[i], ahi[i], 0, 1, 2, 3, 4, 5, 6, 7));
+      for (int j = 0; j < MJ; ++j) {
+        const int col = wc * WCO + 16 * j + 4 * p4;
+        const int r0 = 32 * ks + 8 * g + q4;
+        const s16x4v lo = tr_read(cur + A_BYTES, swz_off<WB>(r0, col));
+        const s16x4v hi = tr_read(cur + A_BYTES, swz_off<WB>(r0 + 4, col));
+        bfr[j] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
 #pragma unroll
-      for (int j = 0; j < MJ; ++j)
-        bfr[j] = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(blo[j], bhi[j], 0, 1, 2, 3, 4, 5, 6, 7));
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < MJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < MJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    if (more) store_stage(smem + ((t + 1) & 1) * STAGE);
+    if constexpr (NST == 2) {
+      if (more) store_stage(smem + ((t + 1) & 1) * STAGE);
+    }
     __syncthreads();
   }
 
-  // ---- intra-block reduction of the 4 waves' partial tiles (each 64 x BC fp32) ----
-  float* red = reinterpret_cast<float*>(smem);  // [3 waves][4][MJ][64 lanes][4]
-  if (wave > 0) {
+  float* out = a.out + (size_t)split * a.K * Ktot;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < MJ; ++j)
-        *reinterpret_cast<f32x4_t*>(red + ((((wave - 1) * 4 + i) * MJ + j) * 64 + lane) * 4) = acc[i][j];
-  }
-  __syncthreads();
-  if (wave == 0) {
-    float* out = a.out + (size_t)split * a.K * Ktot;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < MJ; ++j) {
-        f32x4_t v = acc[i][j];
-#pragma unroll
-        for (int w = 0; w < 3; ++w)
-          v += *reinterpret_cast<const f32x4_t*>(red + (((w * 4 + i) * MJ + j) * 64 + lane) * 4);
-        const int co = c0 + 16 * j + (lane & 15);
-        const int kr = k0 + 16 * i + 4 * (lane >> 4);
-        if (co < a.K && kr < Ktot) *reinterpret_cast<f32x4_t*>(out + (size_t)co * Ktot + kr) = v;
-      }
-  }
+    for (int j = 0; j < MJ; ++j) {
+      const int co = c0 + wc * WCO + 16 * j + (lane & 15);
+      const int kr = k0 + wk * WKK + 16 * i + 4 * (lane >> 4);
+      if (co < a.K && kr < Ktot) *reinterpret_cast<f32x4_t*>(out + (size_t)co * Ktot + kr) = acc[i][j];
+    }
 }
 
-template <int BC, bool PRO>
+template <int BKK, int BCO, bool PRO>
 static int launch_wgrad(DrnConvWgradArgs* a, hipStream_t s) {
-  constexpr int LDS_MAIN = 2 * 2 * 128 * 128;
-  constexpr int LDS_RED = 3 * 4 * (BC / 16) * 64 * 4 * 4;
-  constexpr int LDS = LDS_MAIN > LDS_RED ? LDS_MAIN : LDS_RED;
+  constexpr int NST = DRN_WGRAD_STAGES;
+  constexpr int LDS = NST * (64 * BKK * 2 + 64 * BCO * 2);
   static bool attr_set = false;
-  auto kern = conv_wgrad_kernel<BC, PRO>;
+  auto kern = conv_wgrad_kernel<BKK, BCO, PRO, NST>;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
   }
   const int Ktot = a->R * a->S * a->C;
-  const int nkt = (Ktot + 63) / 64;
-  const int nct = (a->K + BC - 1) / BC;
+  const int nkt = (Ktot + BKK - 1) / BKK;
+  const int nct = (a->K + BCO - 1) / BCO;
   hipLaunchKernelGGL(kern, dim3(nkt * nct, a->splits), dim3(256), LDS, s, *a);
   return (int)hipGetLastError();
+}
+
+template <bool PRO>
+static int dispatch_wgrad(DrnConvWgradArgs* a, hipStream_t s) {
+  const int Ktot = a->R * a->S * a->C;
+  const bool wide_k = Ktot > 64;
+  const bool wide_c = a->K > 64;
+  if (wide_k && wide_c) return launch_wgrad<128, 128, PRO>(a, s);
+  if (wide_k) return launch_wgrad<128, 64, PRO>(a, s);
+  if (wide_c) return launch_wgrad<64, 128, PRO>(a, s);
+  return launch_wgrad<64, 64, PRO>(a, s);
 }
 
 __global__ void splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, int n4, int splits,
@@ -258,12 +277,16 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, float* __rest
 
 }  // namespace drn
 
+// Block-tile shape the dispatcher picks (host mirror used to size the split-K grid).
+DRN_API int drn_wgrad_tiles(int Ktot, int K) {
+  const int bkk = Ktot > 64 ? 128 : 64, bco = K > 64 ? 128 : 64;
+  return ((Ktot + bkk - 1) / bkk) * ((K + bco - 1) / bco);
+}
+
 DRN_API int drn_conv_wgrad(DrnConvWgradArgs* a, hipStream_t s) {
-  if ((a->C % 8) != 0 || (a->K % 8) != 0 || a->splits < 1) return (int)hipErrorInvalidValue;
-  const bool pro = a->in_scale != nullptr;
-  if (a->K >= 64) return pro ? drn::launch_wgrad<64, true>(a, s) : drn::launch_wgrad<64, false>(a, s);
-  if (a->K > 16) return pro ? drn::launch_wgrad<32, true>(a, s) : drn::launch_wgrad<32, false>(a, s);
-  return pro ? drn::launch_wgrad<16, true>(a, s) : drn::launch_wgrad<16, false>(a, s);
+  if ((a->C % 8) != 0 || (a->K % 8) != 0 || a->splits < 1 || (a->pix_per_split % 64) != 0)
+    return (int)hipErrorInvalidValue;
+  return a->in_scale != nullptr ? drn::dispatch_wgrad<true>(a, s) : drn::dispatch_wgrad<false>(a, s);
 }
 
 // out[i] (+)= scale * sum_k ws[k][i]  over n floats (n % 4 == 0), deterministic order.

@@ -109,14 +109,17 @@ class HipBackend(_Common):
         self.launch_conv(self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats))
 
     @staticmethod
-    def wgrad_splits(M, Ktot, K):
-        """Split-K factor over output pixels so the grid has enough workgroups (>= ~2 per CU)."""
-        tiles = ((Ktot + 63) // 64) * ((K + 63) // 64 if K >= 64 else 1)
-        steps = (M + 127) // 128
-        want = max(1, min(steps, (1024 + tiles - 1) // tiles))
+    def wgrad_splits(M, Ktot, K, target_blocks: int = 640, min_steps: int = 8):
+        """Split-K over output pixels: enough workgroups to fill 256 CUs (~2.5 per CU) while
+        keeping >= min_steps 64-pixel steps per split so partial slabs stay cheap."""
+        bkk = 128 if Ktot > 64 else 64
+        bco = 128 if K > 64 else 64
+        tiles = ((Ktot + bkk - 1) // bkk) * ((K + bco - 1) // bco)
+        steps = (M + 63) // 64
+        want = max(1, min((target_blocks + tiles - 1) // tiles, max(1, steps // min_steps)))
         per = (steps + want - 1) // want
         splits = (steps + per - 1) // per
-        return splits, per * 128
+        return splits, per * 64
 
     def wgrad_args(self, x, dy, out, g: ConvGeom, in_bn=None, relu_in=True, ws=None):
         N, H, W, C = x.shape
