@@ -27,7 +27,12 @@ struct DrnConvFwdArgs {
   int32_t N, H, W, C, K, R, S, P, Q;
   int32_t stride, pad_h, pad_w, dil;
   int32_t relu_in;        // 1: relu after the fused scale/shift
-  int32_t tiles_p;        // out: number of pixel tiles (rows of `stats`), filled by the host
+  int32_t tiles_p;        // out: number of pixel tiles, filled by the host
+  // Optional strided output mapping (phase-decomposed data gradient of a stride-2 conv): the
+  // GEMM's P x Q output grid is written to y[n][i*out_stride + out_oh][j*out_stride + out_ow]
+  // of a y tensor of spatial size out_H x out_W (residual uses the same mapping).
+  // out_stride == 0 means the identity mapping (y is [N][P][Q][K]).
+  int32_t out_H, out_W, out_stride, out_oh, out_ow, pad_;
 };
 
 // dW[K][R][S][C] (+)= sum_{n,p,q} dy[n,p,q,k] * x[n, p*st-pad+r, q*st-pad+s, c]

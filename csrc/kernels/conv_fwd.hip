@@ -251,6 +251,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(DrnConvFwdArgs a) {
   const bf16_t* __restrict__ res = reinterpret_cast<const bf16_t*>(a.residual);
   const int ch = tid % CHR;
   const int c = c0 + ch * 8;
+  const bool mapped = a.out_stride != 0;
+  const int pq = a.P * a.Q;
   float ssum[8], ssq[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) ssum[j] = ssq[j] = 0.f;
@@ -262,7 +264,16 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(DrnConvFwdArgs a) {
     const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(tile + row * BC + (((2 * ch + 1) ^ (row & SWM)) * 4));
     if (m < M && c < a.K) {
       float f[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      const size_t off = (size_t)m * a.K + c;
+      size_t off;
+      if (mapped) {
+        const int n = m / pq;
+        const int rem = m - n * pq;
+        const int i = rem / a.Q;
+        const int j = rem - i * a.Q;
+        off = ((size_t)(n * a.out_H + i * a.out_stride + a.out_oh) * a.out_W + j * a.out_stride + a.out_ow) * a.K + c;
+      } else {
+        off = (size_t)m * a.K + c;
+      }
       if (res) {
         float r8[8];
         unpack8(*reinterpret_cast<const uint4*>(res + off), r8);

@@ -41,56 +41,70 @@ __global__ __launch_bounds__(256) void bnrelu_pool_kernel(const bf16_t* __restri
 }
 
 // C[M][N] = alpha * op(A) op(B) + beta * C (+ bias[N]); row-major; op = transpose if flag.
-// 64x64 tile, 256 threads (4x4 outputs each), BK = 16. fp32 (exact, off the MFMA path: the
-// head GEMMs are <1% of the step).
+// Exact-fp32 MFMA (v_mfma_f32_16x16x4_f32, the f32-input matrix path: 16x the VALU-FMA work
+// per instruction, bitwise a k-ordered fmaf chain). 64x64 block tile, 4 waves each 32x32
+// (2x2 MFMA tiles), K staged 32 at a time through LDS ([k][m] and [k][n], +1 padding).
+// Used for the dense layer of the head (logits, dW, dpool: <1 GFLOP each).
 __global__ __launch_bounds__(256) void sgemm_kernel(int ta, int tb, int M, int N, int K, float alpha,
                                                     const float* __restrict__ A, int lda,
                                                     const float* __restrict__ B, int ldb, float beta,
                                                     float* __restrict__ Cm, int ldc, const float* __restrict__ bias) {
-  __shared__ float As[16][64 + 1];
-  __shared__ float Bs[16][64 + 1];
-  const int tx = threadIdx.x % 16, ty = threadIdx.x / 16;
-  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
-  float acc[4][4] = {};
-  for (int k0 = 0; k0 < K; k0 += 16) {
-    for (int t = threadIdx.x; t < 16 * 64; t += 256) {
-      const int kk = t / 64, mm = t % 64;
+  constexpr int BM = 64, BN = 64, BK = 32;
+  __shared__ float As[BK][BM + 1];
+  __shared__ float Bs[BK][BN + 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;
+  f32x4_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < K; k0 += BK) {
+    for (int t = tid; t < BK * BM; t += 256) {
+      int kk, mm;
+      if (ta) { mm = t % BM; kk = t / BM; } else { kk = t % BK; mm = t / BK; }
       const int gm = m0 + mm, gk = k0 + kk;
-      float va = 0.f;
-      if (gm < M && gk < K) va = ta ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk];
-      As[kk][mm] = va;
-      const int gn = n0 + mm;
-      float vb = 0.f;
-      if (gn < N && gk < K) vb = tb ? B[(size_t)gn * ldb + gk] : B[(size_t)gk * ldb + gn];
-      Bs[kk][mm] = vb;
+      float v = 0.f;
+      if (gm < M && gk < K) v = ta ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk];
+      As[kk][mm] = v;
+    }
+    for (int t = tid; t < BK * BN; t += 256) {
+      int kk, nn;
+      if (tb) { kk = t % BK; nn = t / BK; } else { nn = t % BN; kk = t / BN; }
+      const int gn = n0 + nn, gk = k0 + kk;
+      float v = 0.f;
+      if (gn < N && gk < K) v = tb ? B[(size_t)gn * ldb + gk] : B[(size_t)gk * ldb + gn];
+      Bs[kk][nn] = v;
     }
     __syncthreads();
 #pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-      float a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = As[kk][ty * 4 + i];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx * 4 + j];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] += a[i] * b[j];
+    for (int kk = 0; kk < BK; kk += 4) {
+      const int kr = kk + (lane >> 4);
+      float a0 = As[kr][wm + (lane & 15)], a1 = As[kr][wm + 16 + (lane & 15)];
+      float b0 = Bs[kr][wn + (lane & 15)], b1 = Bs[kr][wn + 16 + (lane & 15)];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int gm = m0 + ty * 4 + i, gn = n0 + tx * 4 + j;
-      if (gm < M && gn < N) {
-        float v = alpha * acc[i][j];
-        if (bias) v += bias[gn];
-        if (beta != 0.f) v += beta * Cm[(size_t)gm * ldc + gn];
-        Cm[(size_t)gm * ldc + gn] = v;
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gm = m0 + wm + 16 * i + 4 * (lane >> 4) + r;
+        const int gn = n0 + wn + 16 * j + (lane & 15);
+        if (gm < M && gn < N) {
+          float v = alpha * acc[i][j][r];
+          if (bias) v += bias[gn];
+          if (beta != 0.f) v += beta * Cm[(size_t)gm * ldc + gn];
+          Cm[(size_t)gm * ldc + gn] = v;
+        }
       }
-    }
 }
 
 // One block per sample: softmax, loss, dlogits = (p - y) * grad_scale, correct-count.

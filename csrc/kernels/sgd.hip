@@ -49,12 +49,17 @@ __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict_
   }
 }
 
-// Data-gradient weights: Wt[c][R-1-r][S-1-s][k] = W[k][r][s][c] for a batch of convolutions
-// described by a device-resident table (one launch for the whole network).
+// Data-gradient weights for a batch of convolutions described by a device-resident table (one
+// launch for the whole network): Wt[c][u][v][k] = W[k][r0 + dr*u][s0 + ds*v][c], u < Ru, v < Sv.
+// Full flip (stride-1 data gradient): Ru=R, r0=R-1, dr=-1. Stride-2 data gradients use one
+// sub-kernel per output phase (taps of one parity, dr=-2), so no MFMA work is spent on the
+// zeros of a dilated dY.
 struct TDesc {
-  int64_t src, dst;  // element offsets into the flat bf16 weight buffers
-  int32_t K, R, S, C;
-  int64_t begin;     // prefix sum of element counts (work partition)
+  int64_t src, dst;       // element offsets into the flat bf16 weight buffers
+  int32_t K, R, S, C;     // source KRSC dims
+  int32_t Ru, Sv, r0, s0; // destination taps and first source tap
+  int32_t dr, ds, pad0, pad1;
+  int64_t begin;          // prefix sum of destination element counts (work partition)
 };
 
 __global__ __launch_bounds__(256) void weight_tflip_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt,
@@ -68,12 +73,12 @@ __global__ __launch_bounds__(256) void weight_tflip_kernel(const bf16_t* __restr
       if (table[mid].begin <= i) lo = mid; else hi = mid - 1;
     }
     const TDesc d = table[lo];
-    int64_t e = i - d.begin;  // index into destination [C][R][S][K]
+    int64_t e = i - d.begin;  // index into destination [C][Ru][Sv][K]
     const int k = (int)(e % d.K); e /= d.K;
-    const int s = (int)(e % d.S); e /= d.S;
-    const int r = (int)(e % d.R);
-    const int c = (int)(e / d.R);
-    const int rs = d.R - 1 - r, ssrc = d.S - 1 - s;
+    const int v = (int)(e % d.Sv); e /= d.Sv;
+    const int u = (int)(e % d.Ru);
+    const int c = (int)(e / d.Ru);
+    const int rs = d.r0 + d.dr * u, ssrc = d.s0 + d.ds * v;
     wt[d.dst + i - d.begin] = w[d.src + (((int64_t)k * d.R + rs) * d.S + ssrc) * d.C + c];
   }
 }

@@ -43,6 +43,8 @@ class DrnConvFwdArgs(ctypes.Structure):
         ("N", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("K", c_int), ("R", c_int), ("S", c_int),
         ("P", c_int), ("Q", c_int), ("stride", c_int), ("pad_h", c_int), ("pad_w", c_int), ("dil", c_int),
         ("relu_in", c_int), ("tiles_p", c_int),
+        ("out_H", c_int), ("out_W", c_int), ("out_stride", c_int), ("out_oh", c_int), ("out_ow", c_int),
+        ("pad_", c_int),
     ]
 
 

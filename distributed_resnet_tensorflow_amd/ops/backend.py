@@ -46,14 +46,40 @@ def dgrad_geom(g: ConvGeom, R: int, S: int) -> ConvGeom:
     return ConvGeom(stride=1, pad_h=R - 1 - g.pad_h, pad_w=S - 1 - g.pad_w, dil=g.stride)
 
 
+TDESC = np.dtype([("src", "<i8"), ("dst", "<i8"), ("K", "<i4"), ("R", "<i4"), ("S", "<i4"), ("C", "<i4"),
+                  ("Ru", "<i4"), ("Sv", "<i4"), ("r0", "<i4"), ("s0", "<i4"), ("dr", "<i4"), ("ds", "<i4"),
+                  ("p0", "<i4"), ("p1", "<i4"), ("begin", "<i8")])  # mirror of sgd.hip `struct TDesc`
+
+
+def tflip_desc(src, dst, K, R, S, C, Ru=None, Sv=None, r0=None, s0=None, dr=-1, ds=-1):
+    """Dgrad weight extraction Wt[c][u][v][k] = W[k][r0+dr*u][s0+ds*v][c]; defaults = full flip."""
+    Ru = R if Ru is None else Ru
+    Sv = S if Sv is None else Sv
+    r0 = R - 1 if r0 is None else r0
+    s0 = S - 1 if s0 is None else s0
+    return (src, dst, K, R, S, C, Ru, Sv, r0, s0, dr, ds)
+
+
 def tflip_table(descs):
-    """Pack [(src, dst, K, R, S, C)] element offsets into the int64 device table of
-    drn_weight_tflip (struct TDesc: src, dst, {K,R}, {S,C}, begin)."""
-    rows, begin = [], 0
-    for src, dst, K, R, S, C in descs:
-        rows.append([src, dst, K | (R << 32), S | (C << 32), begin])
-        begin += K * R * S * C
-    return torch.tensor(rows, dtype=torch.int64).view(-1), len(rows), begin
+    """Pack descriptors (see tflip_desc) into the byte table of drn_weight_tflip."""
+    arr = np.zeros(max(1, len(descs)), dtype=TDESC)
+    begin = 0
+    for i, d in enumerate(descs):
+        src, dst, K, R, S, C, Ru, Sv, r0, s0, dr, ds = d
+        arr[i] = (src, dst, K, R, S, C, Ru, Sv, r0, s0, dr, ds, 0, 0, begin)
+        begin += C * Ru * Sv * K
+    return torch.from_numpy(arr.view(np.uint8).copy()), len(descs), begin
+
+
+@dataclass(frozen=True)
+class OutMap:
+    """Strided output mapping of a phase of a stride-2 data gradient: the GEMM's P x Q grid lands
+    at y[:, i*stride + oh, j*stride + ow, :] of the full output tensor."""
+    P: int
+    Q: int
+    stride: int
+    oh: int
+    ow: int
 
 
 # ----------------------------------------------------------------------------------------------
@@ -83,10 +109,13 @@ class HipBackend(_Common):
         return torch.cuda.current_stream(self.device).cuda_stream
 
     # -- conv ---------------------------------------------------------------------------------
-    def conv_args(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None):
+    def conv_args(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None):
         N, H, W, C = x.shape
         K, R, S, C2 = w.shape
         N2, P, Q, K2 = y.shape
+        oH, oW = P, Q
+        if out_map is not None:
+            P, Q = out_map.P, out_map.Q
         assert C == C2 and K == K2 and N == N2, (x.shape, w.shape, y.shape)
         assert x.is_contiguous() and w.is_contiguous() and y.is_contiguous()
         a = _lib.DrnConvFwdArgs()
@@ -98,6 +127,8 @@ class HipBackend(_Common):
         a.N, a.H, a.W, a.C, a.K, a.R, a.S, a.P, a.Q = N, H, W, C, K, R, S, P, Q
         a.stride, a.pad_h, a.pad_w, a.dil = g.stride, g.pad_h, g.pad_w, g.dil
         a.relu_in = 1 if relu_in else 0
+        if out_map is not None:
+            a.out_H, a.out_W, a.out_stride, a.out_oh, a.out_ow = oH, oW, out_map.stride, out_map.oh, out_map.ow
         if stats is not None:
             assert stats.numel() >= 2 * K and stats.dtype == torch.float32, "stats accumulator must be fp32 [2][K]"
         return a
@@ -105,8 +136,8 @@ class HipBackend(_Common):
     def launch_conv(self, a):
         _lib.check(self.L.drn_conv_fwd(ctypes.byref(a), self.stream()), "drn_conv_fwd")
 
-    def conv_fwd(self, x, w, y, g, in_bn=None, relu_in=True, residual=None, stats=None):
-        self.launch_conv(self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats))
+    def conv_fwd(self, x, w, y, g, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None):
+        self.launch_conv(self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats, out_map))
 
     @staticmethod
     def wgrad_splits(M, Ktot, K, target_blocks: int = 640, min_steps: int = 8):
@@ -328,12 +359,21 @@ class RefBackend(_Common):
     def stream(self):
         return None
 
-    def conv_fwd(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None):
+    def conv_fwd(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None):
         K, R, S, C = w.shape
         _, P, Q, _ = y.shape
+        if out_map is not None:
+            P, Q = out_map.P, out_map.Q
         xc = _dilate(_pre(x, in_bn, relu_in).permute(0, 3, 1, 2), g.dil)
         xc = _pad_for(xc, P, Q, R, S, g)
         out = F.conv2d(xc, w.to(_DT[0]).permute(0, 3, 1, 2), stride=g.stride).permute(0, 2, 3, 1)
+        if out_map is not None:
+            sl = (slice(None), slice(out_map.oh, out_map.oh + (P - 1) * out_map.stride + 1, out_map.stride),
+                  slice(out_map.ow, out_map.ow + (Q - 1) * out_map.stride + 1, out_map.stride))
+            if residual is not None:
+                out = out + residual[sl].to(_DT[0])
+            y[sl] = out.to(y.dtype)
+            return
         if residual is not None:
             out = out + residual.to(_DT[0])
         y.copy_(out)
@@ -510,13 +550,15 @@ class RefBackend(_Common):
         y.copy_(x)
 
     def weight_tflip(self, wb, wt, table, ntab, total):
-        for d in table.view(-1, 5).tolist()[:ntab]:
-            src, dst, kr, sc, _begin = d
-            K, R = kr & 0xFFFFFFFF, kr >> 32
-            S, C = sc & 0xFFFFFFFF, sc >> 32
-            n = K * R * S * C
-            w = wb.view(-1)[src:src + n].view(K, R, S, C)
-            wt.view(-1)[dst:dst + n].view(C, R, S, K).copy_(w.flip(1, 2).permute(3, 1, 2, 0))
+        arr = table.cpu().numpy().view(TDESC)[:ntab]
+        for d in arr:
+            src, dst, K, R, S, C = (int(d[k]) for k in ("src", "dst", "K", "R", "S", "C"))
+            Ru, Sv, r0, s0, dr, ds = (int(d[k]) for k in ("Ru", "Sv", "r0", "s0", "dr", "ds"))
+            w = wb.view(-1)[src:src + K * R * S * C].view(K, R, S, C)
+            ridx = torch.tensor([r0 + dr * u for u in range(Ru)])
+            sidx = torch.tensor([s0 + ds * v for v in range(Sv)])
+            sub = w[:, ridx][:, :, sidx]  # K Ru Sv C
+            wt.view(-1)[dst:dst + C * Ru * Sv * K].view(C, Ru, Sv, K).copy_(sub.permute(3, 1, 2, 0))
 
     def zero_(self, t):
         t.zero_()

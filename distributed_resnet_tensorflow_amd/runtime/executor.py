@@ -27,7 +27,7 @@ from typing import Callable, List, Optional
 import torch
 
 from ..models.spec import Block, BN, Conv, NetSpec
-from ..ops.backend import ConvGeom, dgrad_geom, tflip_table
+from ..ops.backend import ConvGeom, OutMap, dgrad_geom, tflip_desc, tflip_table
 from .params import ParamStore
 
 BN_DECAY = 0.997     # reference resnet_model_official.py:37
@@ -57,13 +57,25 @@ class BNState:
 
 
 @dataclass
+class DgradPhase:
+    """One launch of a data gradient: a stride-1 conv of dY with (sub-)kernel `wt`, written to the
+    whole dX (stride-1 convs) or to one output phase of it (stride-2 convs, `out_map`)."""
+    wt_shape: tuple
+    wt_off: int
+    geom: ConvGeom
+    out_map: Optional[OutMap]
+    wt: Optional[torch.Tensor] = None
+
+
+@dataclass
 class ConvOp:
     conv: Conv
     geom: ConvGeom
     w: torch.Tensor        # compute weights [K,R,S,C]
-    wt: Optional[torch.Tensor]  # dgrad weights [C,R,S,K]
+    dg: List[DgradPhase]   # data-gradient launches (empty for the stem)
     dw: torch.Tensor       # fp32 grad view [K,R,S,C]
     grad_lo: int           # flat offset of this conv's gradient slot
+    full_cover: bool = True  # the phases write every dX element
 
 
 @dataclass
@@ -108,17 +120,40 @@ class Executor:
                        P.g(f"{bn.name}/beta"), rm, rv, self._f32(bn.c), self._f32(bn.c), self._f32(bn.c),
                        self._f32(bn.c))
 
-    def _conv_op(self, c: Conv, wt_descs, wt_off) -> tuple[ConvOp, int]:
+    def _conv_op(self, c: Conv, wt_descs, wt_off, in_hw: int = 0) -> tuple[ConvOp, int]:
         P = self.P
         name = f"{c.name}/kernel"
         s = P.by_name[name]
         g = ConvGeom(c.stride, c.pad, c.pad, 1)
-        wt = None
+        phases = []
+        full = True
+        K, R, C = c.cout, c.k, c.cin_store
         if c is not self.spec.stem:
-            wt_descs.append((s.offset, wt_off, c.cout, c.k, c.k, c.cin_store))
-            wt = (c.cin_store, c.k, c.k, c.cout)
-            wt_off += s.numel
-        op = ConvOp(c, g, P.compute_w(name), wt, P.g(name), s.offset)
+            if c.stride == 1:
+                wt_descs.append(tflip_desc(s.offset, wt_off, K, R, R, C))
+                phases.append(DgradPhase((C, R, R, K), wt_off, dgrad_geom(g, R, R), None))
+                wt_off += s.numel
+            else:
+                # phase decomposition of the transposed conv: output parity (ph, pw) only sees the
+                # taps r = ph + pad (mod 2), at dY offsets d = (ph + pad - r) / 2
+                st, p = c.stride, c.pad
+                for ph in range(st):
+                    rs = [r for r in range(R) if (r - ph - p) % st == 0]
+                    for pw in range(st):
+                        ss = [q for q in range(R) if (q - pw - p) % st == 0]
+                        Hph = (in_hw - ph + st - 1) // st
+                        Wph = (in_hw - pw + st - 1) // st
+                        if not rs or not ss or Hph <= 0 or Wph <= 0:
+                            full = False
+                            continue
+                        r0, s0 = max(rs), max(ss)
+                        dmin_h, dmin_w = (ph + p - r0) // st, (pw + p - s0) // st
+                        wt_descs.append(tflip_desc(s.offset, wt_off, K, R, R, C, Ru=len(rs), Sv=len(ss),
+                                                   r0=r0, s0=s0, dr=-st, ds=-st))
+                        phases.append(DgradPhase((C, len(rs), len(ss), K), wt_off,
+                                                 ConvGeom(1, -dmin_h, -dmin_w, 1), OutMap(Hph, Wph, st, ph, pw)))
+                        wt_off += C * len(rs) * len(ss) * K
+        op = ConvOp(c, g, P.compute_w(name), phases, P.g(name), s.offset, full)
         return op, wt_off
 
     def _stats_for(self, M: int, C: int) -> tuple[torch.Tensor, int]:
@@ -153,13 +188,14 @@ class Executor:
             bns[0].stats, bns[0].G = x_stats, x_G
             bns[0].rows = x.numel() // blk.in_c
             convs = []
+            h_in = blk.in_hw
             for c in blk.convs:
-                op, wt_off = None, wt_off
-                op, wt_off = self._conv_op(c, wt_descs, wt_off)
+                op, wt_off = self._conv_op(c, wt_descs, wt_off, in_hw=h_in)
                 convs.append(op)
+                h_in = c.out_hw(h_in)
             proj = None
             if blk.proj is not None:
-                proj, wt_off = self._conv_op(blk.proj, wt_descs, wt_off)
+                proj, wt_off = self._conv_op(blk.proj, wt_descs, wt_off, in_hw=blk.in_hw)
             # main-path intermediate outputs + their stats (feeding bn2/bn3)
             h_list = []
             hw = blk.in_hw
@@ -220,10 +256,11 @@ class Executor:
         table, nt, total = tflip_table(wt_descs)
         self.wt_table, self.wt_n, self.wt_total = table.to(self.device), nt, total
         for op in self._all_ops():
-            if op.wt is not None:
-                src = self.P.by_name[f"{op.conv.name}/kernel"].offset
-                d = next(d for d in wt_descs if d[0] == src)
-                op.wt = self.wt_flat[d[1]:d[1] + op.dw.numel()].view(op.wt)
+            for ph in op.dg:
+                n = 1
+                for d in ph.wt_shape:
+                    n *= d
+                ph.wt = self.wt_flat[ph.wt_off:ph.wt_off + n].view(ph.wt_shape)
         self.lr_t = self._f32(1)
 
     def _all_ops(self):
@@ -346,6 +383,12 @@ class Executor:
         if self.grad_ready is not None:
             self.grad_ready(0)
 
+    def _dgrad(self, op: ConvOp, dy, dx, accumulate: bool):
+        if not accumulate and not op.full_cover:
+            self.be.zero_(dx)
+        for ph in op.dg:
+            self.be.conv_fwd(dy, ph.wt, dx, ph.geom, residual=dx if accumulate else None, out_map=ph.out_map)
+
     def _block_bwd(self, bp: BlockPlan, bufs, cur: int) -> int:
         """Back-propagates one block; bufs[cur] holds d(block output). Returns the index of the
         buffer holding d(block input). Two free buffers alternate: the dgrad of conv i writes the
@@ -360,13 +403,13 @@ class Executor:
             tgt = free[0] if dy_buf is not free[0] else free[1]
             be.conv_wgrad(xin, dy, op.dw, op.geom, in_bn=b.ss, ws=self.wgrad_ws)
             da = self._view(tgt, xin)        # d relu(bn(xin))
-            be.conv_fwd(dy, op.wt, da, dgrad_geom(op.geom, op.conv.k, op.conv.k))
+            self._dgrad(op, dy, da, accumulate=False)
             add = None
             if i == 0:
                 if bp.proj is not None:
                     pj = bp.proj
                     be.conv_wgrad(bp.x, d_out, pj.dw, pj.geom, in_bn=b.ss, ws=self.wgrad_ws)
-                    be.conv_fwd(d_out, pj.wt, da, dgrad_geom(pj.geom, 1, 1), residual=da)
+                    self._dgrad(pj, d_out, da, accumulate=True)
                 else:
                     add = d_out              # identity shortcut
             self._bn_bwd(b, xin, da, da, add=add)

@@ -7,7 +7,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from distributed_resnet_tensorflow_amd.ops.backend import ConvGeom, dgrad_geom, tflip_table
+from distributed_resnet_tensorflow_amd.ops.backend import ConvGeom, dgrad_geom, tflip_desc, tflip_table
 
 pytestmark = pytest.mark.gpu
 
@@ -280,8 +280,9 @@ def test_sgd_and_tflip(hip, ref):
     for a, b in zip(res["hip"], res["ref"]):
         assert rel(a, b) < 4e-3
     # transpose-flip
-    descs = [(0, 0, 16, 3, 3, 8), (16 * 9 * 8, 16 * 9 * 8, 32, 1, 1, 16)]
-    tot = 16 * 9 * 8 + 32 * 16
+    descs = [tflip_desc(0, 0, 16, 3, 3, 8), tflip_desc(16 * 9 * 8, 16 * 9 * 8, 32, 1, 1, 16),
+             tflip_desc(0, 16 * 9 * 8 + 32 * 16, 16, 3, 3, 8, Ru=2, Sv=1, r0=2, s0=1, dr=-2, ds=-2)]
+    tot = 16 * 9 * 8 + 32 * 16 + 16 * 2 * 8
     wflat = torch.randn(tot)
     table, nt, total = tflip_table(descs)
     out_ref = torch.zeros(tot)
