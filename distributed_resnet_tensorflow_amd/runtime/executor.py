@@ -50,6 +50,8 @@ class BNState:
     stats: Optional[torch.Tensor] = None  # partial stats of the normalised tensor [G][2][C]
     G: int = 1
     rows: int = 0                          # N*H*W of the normalised tensor
+    src: Optional[torch.Tensor] = None     # the raw (pre-BN) tensor
+    act: Optional[torch.Tensor] = None     # materialised relu(bn(src)) (materialize_bn mode)
 
     @property
     def ss(self):
@@ -93,11 +95,20 @@ class BlockPlan:
 
 class Executor:
     def __init__(self, spec: NetSpec, batch: int, backend, device, seed: int = 0,
-                 weight_decay: float = 2e-4, momentum: float = 0.9, params: ParamStore | None = None):
+                 weight_decay: float = 2e-4, momentum: float = 0.9, params: ParamStore | None = None,
+                 materialize_bn: Optional[bool] = None):
         self.spec, self.N, self.be = spec, batch, backend
         self.device = torch.device(device)
         self.wd, self.mom = weight_decay, momentum
         self.is_hip = backend.name == "hip"
+        # BN-apply+ReLU either fused into every consuming conv's load prologue (recomputed by the
+        # forward conv, the projection conv and both weight-gradient convs) or materialised once
+        # per BN by a streaming kernel (one extra read+write of the tensor, no per-element VALU
+        # work in the MFMA loops). Measured on MI355X the materialised form is faster.
+        if materialize_bn is None:
+            import os
+            materialize_bn = os.environ.get("DRN_FUSE_BN_PROLOGUE", "0") != "1"
+        self.materialize_bn = materialize_bn
         self.fdt = backend.acc_dtype
         self.P = params or ParamStore(spec, self.device, keep_bf16=self.is_hip, seed=seed, dtype=self.fdt)
         self.grad_ready: Optional[Callable[[int], None]] = None
@@ -187,6 +198,7 @@ class Executor:
             bns = [self._bn_state(blk.bn1)] + [self._bn_state(b) for b in blk.bns]
             bns[0].stats, bns[0].G = x_stats, x_G
             bns[0].rows = x.numel() // blk.in_c
+            bns[0].src = x
             convs = []
             h_in = blk.in_hw
             for c in blk.convs:
@@ -205,6 +217,7 @@ class Executor:
                 st, G = self._stats_for(N * hw * hw, c.cout)
                 bns[i + 1].stats, bns[i + 1].G = st, G
                 bns[i + 1].rows = N * hw * hw
+                bns[i + 1].src = h
                 h_list.append(h)
                 max_act = max(max_act, h.numel())
             ohw = blk.out_hw
@@ -231,6 +244,11 @@ class Executor:
         self.final_bn = self._bn_state(sp.final_bn)
         self.final_bn.stats, self.final_bn.G = x_stats, x_G
         self.final_bn.rows = x.numel() // sp.final_c
+        self.final_bn.src = x
+        if self.materialize_bn:
+            for bp in self.blocks:
+                for b in bp.bn:
+                    b.act = self._act(*b.src.shape)
         self.last_out = x
         C, ncls = sp.final_c, sp.num_classes
         self.pooled = self._f32(N, C)
@@ -294,6 +312,13 @@ class Executor:
         else:
             self.be.bn_inference(b.gamma, b.beta, b.run_mean, b.run_var, BN_EPSILON, b.scale, b.shift, b.mean,
                                  b.invstd)
+        if b.act is not None:
+            self.be.bn_apply(b.src, b.act, b.scale, b.shift, relu=True)
+
+    @staticmethod
+    def _cin(b: BNState):
+        """(tensor, in_bn) a conv consuming relu(bn(b.src)) reads."""
+        return (b.act, None) if b.act is not None else (b.src, b.ss)
 
     def forward(self, train: bool = True):
         """Runs the network on self.images/self.labels; fills loss_vec/correct (and dlogits)."""
@@ -321,19 +346,19 @@ class Executor:
         bn = bp.bn
         self._bn_fwd(bn[0], train)
         if bp.proj is not None:
-            be.conv_fwd(bp.x, bp.proj.w, bp.sc, bp.proj.geom, in_bn=bn[0].ss)
-        inp = bp.x
+            xin, pro = self._cin(bn[0])
+            be.conv_fwd(xin, bp.proj.w, bp.sc, bp.proj.geom, in_bn=pro)
         for i, op in enumerate(bp.convs):
             last = i == len(bp.convs) - 1
+            xin, pro = self._cin(bn[i])
             if last:
                 res = bp.sc if bp.proj is not None else bp.x
-                be.conv_fwd(inp, op.w, bp.out, op.geom, in_bn=bn[i].ss, residual=res,
+                be.conv_fwd(xin, op.w, bp.out, op.geom, in_bn=pro, residual=res,
                             stats=bp.out_stats if train else None)
             else:
-                be.conv_fwd(inp, op.w, bp.hs[i], op.geom, in_bn=bn[i].ss,
+                be.conv_fwd(xin, op.w, bp.hs[i], op.geom, in_bn=pro,
                             stats=bn[i + 1].stats if train else None)
                 self._bn_fwd(bn[i + 1], train)
-                inp = bp.hs[i]
 
     # ------------------------------------------------------------------------------------------
     # backward
@@ -401,14 +426,15 @@ class Executor:
         for i in reversed(range(len(bp.convs))):
             op, xin, b = bp.convs[i], ins[i], bp.bn[i]
             tgt = free[0] if dy_buf is not free[0] else free[1]
-            be.conv_wgrad(xin, dy, op.dw, op.geom, in_bn=b.ss, ws=self.wgrad_ws)
+            a_in, pro = self._cin(b)
+            be.conv_wgrad(a_in, dy, op.dw, op.geom, in_bn=pro, ws=self.wgrad_ws)
             da = self._view(tgt, xin)        # d relu(bn(xin))
             self._dgrad(op, dy, da, accumulate=False)
             add = None
             if i == 0:
                 if bp.proj is not None:
                     pj = bp.proj
-                    be.conv_wgrad(bp.x, d_out, pj.dw, pj.geom, in_bn=b.ss, ws=self.wgrad_ws)
+                    be.conv_wgrad(a_in, d_out, pj.dw, pj.geom, in_bn=pro, ws=self.wgrad_ws)
                     self._dgrad(pj, d_out, da, accumulate=True)
                 else:
                     add = d_out              # identity shortcut

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--json", default="")
+    ap.add_argument("--only", default="", help="substring filter on the layer name (e.g. 'conv 256->256 k3s1')")
     a = ap.parse_args()
     spec = build_spec(a.dataset, a.resnet_size)
     be = HipBackend()
@@ -60,6 +61,8 @@ def main():
     rows = []
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0, "bn_bwd": 0.0}
     for (kind, cin, cout, k, s, H), cnt in shapes.items():
+        if a.only and a.only not in f"{kind} {cin}->{cout} k{k}s{s} @{H}":
+            continue
         P = H if s == 1 else (H - 1) // s + 1
         g = ConvGeom(s, (k - 1) // 2, (k - 1) // 2)
         x = torch.randn(N, H, H, cin, device="cuda").bfloat16()
