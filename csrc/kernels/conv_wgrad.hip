@@ -258,20 +258,52 @@ static int dispatch_wgrad(DrnConvWgradArgs* a, hipStream_t s) {
   return launch_wgrad<64, 64, PRO>(a, s);
 }
 
-__global__ void splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out, int n4, int splits,
-                                     size_t stride4, float scale, int accumulate) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
-    float4 s = reinterpret_cast<const float4*>(ws)[i];
-    for (int k = 1; k < splits; ++k) {
-      const float4 v = reinterpret_cast<const float4*>(ws)[i + k * stride4];
-      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+// out[i] (+)= scale * sum_k ws[k][i]: block = 64 float4 columns x 4 split-groups; every
+// thread keeps 4 independent loads in flight (the split loop is the latency chain for small
+// tensors with many splits), then the 4 groups are summed through LDS in a fixed order
+// (deterministic).
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out,
+                                                            int n4, int splits, size_t stride4, float scale,
+                                                            int accumulate) {
+  __shared__ float4 red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + tx;
+  float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, s3 = s0;
+  if (i < n4) {
+    const float4* p = reinterpret_cast<const float4*>(ws) + i;
+    int k = ty;
+    for (; k + 12 < splits; k += 16) {
+      const float4 a = p[(size_t)k * stride4], b = p[(size_t)(k + 4) * stride4];
+      const float4 c = p[(size_t)(k + 8) * stride4], d = p[(size_t)(k + 12) * stride4];
+      s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+      s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
+      s2.x += c.x; s2.y += c.y; s2.z += c.z; s2.w += c.w;
+      s3.x += d.x; s3.y += d.y; s3.z += d.z; s3.w += d.w;
     }
-    s.x *= scale; s.y *= scale; s.z *= scale; s.w *= scale;
+    for (; k < splits; k += 4) {
+      const float4 a = p[(size_t)k * stride4];
+      s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+    }
+  }
+  float4 t;
+  t.x = (s0.x + s1.x) + (s2.x + s3.x);
+  t.y = (s0.y + s1.y) + (s2.y + s3.y);
+  t.z = (s0.z + s1.z) + (s2.z + s3.z);
+  t.w = (s0.w + s1.w) + (s2.w + s3.w);
+  red[ty][tx] = t;
+  __syncthreads();
+  if (ty == 0 && i < n4) {
+    float4 r = red[0][tx];
+#pragma unroll
+    for (int g = 1; g < 4; ++g) {
+      r.x += red[g][tx].x; r.y += red[g][tx].y; r.z += red[g][tx].z; r.w += red[g][tx].w;
+    }
+    r.x *= scale; r.y *= scale; r.z *= scale; r.w *= scale;
     if (accumulate) {
       const float4 o = reinterpret_cast<float4*>(out)[i];
-      s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
+      r.x += o.x; r.y += o.y; r.z += o.z; r.w += o.w;
     }
-    reinterpret_cast<float4*>(out)[i] = s;
+    reinterpret_cast<float4*>(out)[i] = r;
   }
 }
 
@@ -294,10 +326,8 @@ DRN_API int drn_splitk_reduce(const float* ws, float* out, int64_t n, int splits
                               hipStream_t s) {
   if (n % 4) return (int)hipErrorInvalidValue;
   const int n4 = (int)(n / 4);
-  int blocks = (n4 + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(drn::splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, out, n4, splits, (size_t)n4,
-                     scale, accumulate);
+  const int blocks = (n4 + 63) / 64;
+  hipLaunchKernelGGL(drn::splitk_reduce_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, s, ws, out, n4, splits,
+                     (size_t)n4, scale, accumulate);
   return (int)hipGetLastError();
 }

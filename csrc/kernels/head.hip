@@ -55,18 +55,28 @@ __global__ __launch_bounds__(256) void sgemm_kernel(int ta, int tb, int M, int N
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;
+  // split-K over gridDim.z: slice z sums k in [kb, ke) and writes its partial tile to
+  // Cm + z * M * ldc (beta/bias are then applied by sgemm_finish_kernel)
+  const int ksz = (((K + gridDim.z - 1) / gridDim.z) + BK - 1) / BK * BK;
+  const int kb = blockIdx.z * ksz, ke = min(K, kb + ksz);
+  if (gridDim.z > 1) {
+    Cm += (size_t)blockIdx.z * M * ldc;
+    beta = 0.f;
+    bias = nullptr;
+    alpha = 1.f;
+  }
   f32x4_t acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = 0; k0 < K; k0 += BK) {
+  for (int k0 = kb; k0 < ke; k0 += BK) {
     for (int t = tid; t < BK * BM; t += 256) {
       int kk, mm;
       if (ta) { mm = t % BM; kk = t / BM; } else { kk = t % BK; mm = t / BK; }
       const int gm = m0 + mm, gk = k0 + kk;
       float v = 0.f;
-      if (gm < M && gk < K) v = ta ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk];
+      if (gm < M && gk < ke) v = ta ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk];
       As[kk][mm] = v;
     }
     for (int t = tid; t < BK * BN; t += 256) {
@@ -74,7 +84,7 @@ __global__ __launch_bounds__(256) void sgemm_kernel(int ta, int tb, int M, int N
       if (tb) { kk = t % BK; nn = t / BK; } else { nn = t % BN; kk = t / BN; }
       const int gn = n0 + nn, gk = k0 + kk;
       float v = 0.f;
-      if (gn < N && gk < K) v = tb ? B[(size_t)gn * ldb + gk] : B[(size_t)gk * ldb + gn];
+      if (gn < N && gk < ke) v = tb ? B[(size_t)gn * ldb + gk] : B[(size_t)gk * ldb + gn];
       Bs[kk][nn] = v;
     }
     __syncthreads();
@@ -105,6 +115,20 @@ __global__ __launch_bounds__(256) void sgemm_kernel(int ta, int tb, int M, int N
           Cm[(size_t)gm * ldc + gn] = v;
         }
       }
+}
+
+// C = alpha * sum_z ws[z] + beta * C (+ bias), fixed summation order (deterministic).
+__global__ void sgemm_finish_kernel(const float* __restrict__ ws, int splits, int M, int N, int ldc, float alpha,
+                                    float beta, float* __restrict__ Cm, const float* __restrict__ bias) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * N) return;
+  const int m = idx / N, n = idx - m * N;
+  float s = 0.f;
+  for (int z = 0; z < splits; ++z) s += ws[(size_t)z * M * ldc + (size_t)m * ldc + n];
+  float v = alpha * s;
+  if (bias) v += bias[n];
+  if (beta != 0.f) v += beta * Cm[(size_t)m * ldc + n];
+  Cm[(size_t)m * ldc + n] = v;
 }
 
 // One block per sample: softmax, loss, dlogits = (p - y) * grad_scale, correct-count.
@@ -178,11 +202,17 @@ DRN_API int drn_bnrelu_pool(const void* x, const float* scale, const float* shif
   return (int)hipGetLastError();
 }
 
+// splits > 1 needs ws with room for splits * M * ldc floats.
 DRN_API int drn_sgemm(int ta, int tb, int M, int N, int K, float alpha, const float* A, int lda, const float* B,
-                      int ldb, float beta, float* C, int ldc, const float* bias, hipStream_t s) {
-  dim3 grid((N + 63) / 64, (M + 63) / 64);
-  hipLaunchKernelGGL(drn::sgemm_kernel, grid, dim3(256), 0, s, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc,
-                     bias);
+                      int ldb, float beta, float* C, int ldc, const float* bias, int splits, float* ws,
+                      hipStream_t s) {
+  if (splits < 1 || (splits > 1 && ws == nullptr)) return (int)hipErrorInvalidValue;
+  dim3 grid((N + 63) / 64, (M + 63) / 64, splits);
+  hipLaunchKernelGGL(drn::sgemm_kernel, grid, dim3(256), 0, s, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta,
+                     splits > 1 ? ws : C, ldc, bias);
+  if (splits > 1)
+    hipLaunchKernelGGL(drn::sgemm_finish_kernel, dim3((M * N + 255) / 256), dim3(256), 0, s, ws, splits, M, N, ldc,
+                       alpha, beta, C, bias);
   return (int)hipGetLastError();
 }
 

@@ -71,7 +71,8 @@ _SIGS = {
     "drn_bn_finalize_bwd": ([c_p, c_int, c_int, c_f, c_p, c_p, c_p, c_p, c_p, c_p], c_int),
     "drn_bn_bwd_apply": ([c_p, c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_p], c_int),
     "drn_bnrelu_pool": ([c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p], c_int),
-    "drn_sgemm": ([c_int, c_int, c_int, c_int, c_int, c_f, c_p, c_int, c_p, c_int, c_f, c_p, c_int, c_p, c_p], c_int),
+    "drn_sgemm": ([c_int, c_int, c_int, c_int, c_int, c_f, c_p, c_int, c_p, c_int, c_f, c_p, c_int, c_p, c_int, c_p,
+                   c_p], c_int),
     "drn_softmax_xent": ([c_p, c_p, c_int, c_int, c_f, c_p, c_p, c_p, c_p, c_p], c_int),
     "drn_colsum": ([c_p, c_int, c_int, c_p, c_f, c_int, c_p], c_int),
     "drn_maxpool_fwd": ([c_p, c_p, c_p] + [c_int] * 10 + [c_p], c_int),

@@ -254,9 +254,21 @@ class HipBackend(_Common):
         _lib.check(self.L.drn_bnrelu_pool(x.data_ptr(), _ptr(scale), _ptr(shift), pooled.data_ptr(), N, H * W, C,
                                           1 if relu else 0, self.stream()), "drn_bnrelu_pool")
 
+    _sgemm_ws = None
+
     def sgemm(self, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias=None):
+        tiles = ((M + 63) // 64) * ((N + 63) // 64)
+        splits = max(1, min(K // 128, 256 // max(tiles, 1)))  # fill >= ~256 CUs on long-K GEMMs
+        ws = None
+        if splits > 1:
+            need = splits * M * ldc
+            if HipBackend._sgemm_ws is None or HipBackend._sgemm_ws.numel() < need \
+                    or HipBackend._sgemm_ws.device != C.device:
+                HipBackend._sgemm_ws = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=C.device)
+            ws = HipBackend._sgemm_ws
         _lib.check(self.L.drn_sgemm(int(ta), int(tb), M, N, K, float(alpha), A.data_ptr(), lda, B.data_ptr(), ldb,
-                                    float(beta), C.data_ptr(), ldc, _ptr(bias), self.stream()), "drn_sgemm")
+                                    float(beta), C.data_ptr(), ldc, _ptr(bias), splits, _ptr(ws), self.stream()),
+                   "drn_sgemm")
 
     def softmax_xent(self, logits, labels, grad_scale, dlogits, loss, correct, probs=None):
         N, ncls = logits.shape
