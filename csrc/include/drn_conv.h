@@ -32,7 +32,10 @@ struct DrnConvFwdArgs {
   // GEMM's P x Q output grid is written to y[n][i*out_stride + out_oh][j*out_stride + out_ow]
   // of a y tensor of spatial size out_H x out_W (residual uses the same mapping).
   // out_stride == 0 means the identity mapping (y is [N][P][Q][K]).
-  int32_t out_H, out_W, out_stride, out_oh, out_ow, pad_;
+  int32_t out_H, out_W, out_stride, out_oh, out_ow;
+  // Kernel configuration for drn_conv_fwd2: -1 automatic, 0..7 an LDS-DMA tile configuration
+  // (DRN_GLDS_CONFIGS), 100 the register-staged kernel.
+  int32_t cfg;
 };
 
 // dW[K][R][S][C] (+)= sum_{n,p,q} dy[n,p,q,k] * x[n, p*st-pad+r, q*st-pad+s, c]

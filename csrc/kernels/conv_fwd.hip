@@ -25,6 +25,98 @@
 
 namespace drn {
 
+// ---------------- shared epilogue ----------------
+// The fp32 accumulator tile is staged through LDS ([BP][BC] fp32, 16-byte chunks XOR-swizzled
+// by row: conflict-free 8-lane ds_write_b128 groups and 16-lane ds_read_b128 groups), then
+// every lane owns 8 consecutive channels of one pixel: 16-byte residual loads and 16-byte
+// bf16 stores, whole 2*BC-byte pixel rows per wave instruction (fully coalesced). Optional
+// residual add, optional strided output map, optional per-channel sum/sumsq for the next BN.
+template <int BP, int BC, int WP, int WC, int MI, int MJ>
+__device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* smem, f32x4_t (&acc)[MI][MJ], int wp,
+                                              int wc, int m0, int c0, int M) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  constexpr int CF = BC / 4;   // fp32 16-byte chunks per staged row
+  constexpr int CHR = BC / 8;  // output 16-byte (8 x bf16) chunks per pixel row
+  constexpr int RPI = 256 / CHR;
+  constexpr int SWM = CF >= 8 ? 7 : CF - 1;  // swizzle mask stays inside a staged row
+  float* tile = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int cf = (wc * WC + i * 16) / 4 + (lane >> 4);  // fp32 chunk of these 4 channels
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) {
+      const int row = wp * WP + j * 16 + (lane & 15);
+      *reinterpret_cast<f32x4_t*>(tile + row * BC + ((cf ^ (row & SWM)) * 4)) = acc[i][j];
+    }
+  }
+  __syncthreads();
+  const bool want_stats = a.stats != nullptr;
+  bf16_t* __restrict__ y = reinterpret_cast<bf16_t*>(a.y);
+  const bf16_t* __restrict__ res = reinterpret_cast<const bf16_t*>(a.residual);
+  const int ch = tid % CHR;
+  const int c = c0 + ch * 8;
+  const bool mapped = a.out_stride != 0;
+  const int pq = a.P * a.Q;
+  float ssum[8], ssq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ssum[j] = ssq[j] = 0.f;
+#pragma unroll
+  for (int it = 0; it < BP / RPI; ++it) {
+    const int row = it * RPI + tid / CHR;
+    const int m = m0 + row;
+    const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(tile + row * BC + (((2 * ch) ^ (row & SWM)) * 4));
+    const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(tile + row * BC + (((2 * ch + 1) ^ (row & SWM)) * 4));
+    if (m < M && c < a.K) {
+      float f[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      size_t off;
+      if (mapped) {
+        const int n = m / pq;
+        const int rem = m - n * pq;
+        const int i = rem / a.Q;
+        const int j = rem - i * a.Q;
+        off = ((size_t)(n * a.out_H + i * a.out_stride + a.out_oh) * a.out_W + j * a.out_stride + a.out_ow) * a.K + c;
+      } else {
+        off = (size_t)m * a.K + c;
+      }
+      if (res) {
+        float r8[8];
+        unpack8(*reinterpret_cast<const uint4*>(res + off), r8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] += r8[j];
+      }
+      const uint4 o = pack8(f);
+      *reinterpret_cast<uint4*>(y + off) = o;
+      if (want_stats) {
+        float q8[8];
+        unpack8(o, q8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ssum[j] += q8[j];
+          ssq[j] += q8[j] * q8[j];
+        }
+      }
+    }
+  }
+  if (want_stats) {
+    __syncthreads();
+    float* red = tile;  // [256][16]
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[tid * 16 + j] = ssum[j];
+      red[tid * 16 + 8 + j] = ssq[j];
+    }
+    __syncthreads();
+    if (tid < 2 * BC) {
+      const int cl = tid >> 1, which = tid & 1;
+      const int chh = cl >> 3, j = cl & 7;
+      float s = 0.f;
+      for (int t2 = chh; t2 < 256; t2 += CHR) s += red[t2 * 16 + which * 8 + j];
+      if (c0 + cl < a.K) atomicAdd(a.stats + (size_t)which * a.K + c0 + cl, s);
+    }
+  }
+}
+
 template <int BP, int BC, int BK, int WP, int WC, bool PRO, bool DIL2>
 __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(DrnConvFwdArgs a) {
   constexpr int CH = BK / 8;                  // 16-byte chunks per row per stage
@@ -225,91 +317,240 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(DrnConvFwdArgs a) {
     __syncthreads();
   }
 
-  // ---------------- epilogue ----------------
-  // The fp32 accumulator tile is staged through LDS ([BP][BC] fp32, 16-byte chunks XOR-swizzled
-  // by row: conflict-free 8-lane ds_write_b128 groups and 16-lane ds_read_b128 groups), then
-  // every lane owns 8 consecutive channels of one pixel: 16-byte residual loads and 16-byte
-  // bf16 stores, whole 2*BC-byte pixel rows per wave instruction (fully coalesced).
-  constexpr int CF = BC / 4;   // fp32 16-byte chunks per staged row
-  constexpr int CHR = BC / 8;  // output 16-byte (8 x bf16) chunks per pixel row
-  constexpr int RPI = 256 / CHR;
-  constexpr int SWM = CF >= 8 ? 7 : CF - 1;  // swizzle mask stays inside a staged row
   static_assert(BP * BC * 4 <= 2 * STAGE, "epilogue tile must fit the staging LDS");
-  float* tile = reinterpret_cast<float*>(smem);
+  conv_epilogue<BP, BC, WP, WC, MI, MJ>(a, smem, acc, wp, wc, m0, c0, M);
+}
+
+// ---------------------------------------------------------------------------------------
+// LDS-DMA pipelined variant (C % 64 == 0, no fused prologue, dil 1): the main path of every
+// ResNet convolution except the 8-channel stem and the narrow CIFAR stages.
+//
+// Operand tiles go global -> LDS directly with `global_load_lds_dwordx4` (no VGPR staging, no
+// ds_write pass), NS LDS stages deep: stage t+NS-1 is in flight while stage t computes, retired
+// by a counted `s_waitcnt vmcnt` + raw `s_barrier` (a __syncthreads() would drain the DMA
+// queue). A stage is one 64-deep slice of k = (r, s, ci): since C % 64 == 0 it lies inside a
+// single filter tap, so the tap / channel offset is wave-uniform and every lane only adds its
+// pixel base; out-of-image taps and out-of-range rows read a 16-byte zero page (no branches).
+// LDS image per stage: [BC + BP rows][128 B], 16-byte chunk j of row r stored at slot
+// j ^ ((r >> 1) & 7) — the swizzle is applied on the per-lane SOURCE address (an LDS-DMA
+// writes lane-linear), and makes the 16x16x32 fragment reads (ds_read_b128, 4 lane groups)
+// bank-conflict free (checked exhaustively against the gfx950 lane-group table).
+// ---------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void drn_lds_void;
+typedef __attribute__((address_space(1))) const void drn_gbl_void;
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_base) {
+  __builtin_amdgcn_global_load_lds((drn_gbl_void*)src, (drn_lds_void*)lds_base, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BP, int BC, int WAVES_P, int NS>
+__global__ __launch_bounds__(256) void conv_fwd_glds_kernel(DrnConvFwdArgs a, const void* __restrict__ zero) {
+  constexpr int WAVES_C = 4 / WAVES_P;
+  constexpr int WP = BP / WAVES_P, WC = BC / WAVES_C;
+  constexpr int MI = WC / 16, MJ = WP / 16;
+  constexpr int ROWB = 128;                 // 64 bf16 of k per LDS row
+  constexpr int STAGE = (BC + BP) * ROWB;
+  constexpr int GA = BC / 32, GB = BP / 32;  // glds wave-instructions per stage (8 rows each)
+  constexpr int G = GA + GB;
+  constexpr int D = NS - 1;                 // stages in flight ahead of the computing one
+  static_assert(WAVES_P * WAVES_C == 4 && MI >= 1 && MJ >= 1, "4 waves");
+  static_assert(NS >= 2 && G * (D > 1 ? D - 1 : 1) < 64, "pipeline depth");
+
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int M = a.N * a.P * a.Q;
+  const int C = a.C;
+  const int Ktot = a.R * a.S * C;
+  const int ntc = (a.K + BC - 1) / BC;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tc = bid % ntc;
+  const int tp = bid / ntc;
+  const int m0 = tp * BP;
+  const int c0 = tc * BC;
+
+  // ---- per-lane loader state ----
+  const int lrow = lane >> 3;
+  const bf16_t* __restrict__ xg = reinterpret_cast<const bf16_t*>(a.x);
+  const bf16_t* wsrc[GA];
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const int cf = (wc * WC + i * 16) / 4 + (lane >> 4);  // fp32 chunk of these 4 channels
-#pragma unroll
-    for (int j = 0; j < MJ; ++j) {
-      const int row = wp * WP + j * 16 + (lane & 15);
-      *reinterpret_cast<f32x4_t*>(tile + row * BC + ((cf ^ (row & SWM)) * 4)) = acc[i][j];
-    }
+  for (int i = 0; i < GA; ++i) {
+    const int row = 32 * i + 8 * wave + lrow;
+    const int lc = (lane & 7) ^ ((row >> 1) & 7);
+    const int c = c0 + row;
+    wsrc[i] = c < a.K ? reinterpret_cast<const bf16_t*>(a.w) + (size_t)c * Ktot + lc * 8 : nullptr;
   }
-  __syncthreads();
-  const bool want_stats = a.stats != nullptr;
-  bf16_t* __restrict__ y = reinterpret_cast<bf16_t*>(a.y);
-  const bf16_t* __restrict__ res = reinterpret_cast<const bf16_t*>(a.residual);
-  const int ch = tid % CHR;
-  const int c = c0 + ch * 8;
-  const bool mapped = a.out_stride != 0;
-  const int pq = a.P * a.Q;
-  float ssum[8], ssq[8];
+  int boff[GB], bh[GB], bw[GB];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) ssum[j] = ssq[j] = 0.f;
-#pragma unroll
-  for (int it = 0; it < BP / RPI; ++it) {
-    const int row = it * RPI + tid / CHR;
+  for (int i = 0; i < GB; ++i) {
+    const int row = 32 * i + 8 * wave + lrow;
+    const int lc = (lane & 7) ^ ((row >> 1) & 7);  // (BC + row) has the same bits 1..3
     const int m = m0 + row;
-    const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(tile + row * BC + (((2 * ch) ^ (row & SWM)) * 4));
-    const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(tile + row * BC + (((2 * ch + 1) ^ (row & SWM)) * 4));
-    if (m < M && c < a.K) {
-      float f[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      size_t off;
-      if (mapped) {
-        const int n = m / pq;
-        const int rem = m - n * pq;
-        const int i = rem / a.Q;
-        const int j = rem - i * a.Q;
-        off = ((size_t)(n * a.out_H + i * a.out_stride + a.out_oh) * a.out_W + j * a.out_stride + a.out_ow) * a.K + c;
-      } else {
-        off = (size_t)m * a.K + c;
-      }
-      if (res) {
-        float r8[8];
-        unpack8(*reinterpret_cast<const uint4*>(res + off), r8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] += r8[j];
-      }
-      const uint4 o = pack8(f);
-      *reinterpret_cast<uint4*>(y + off) = o;
-      if (want_stats) {
-        float q8[8];
-        unpack8(o, q8);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          ssum[j] += q8[j];
-          ssq[j] += q8[j] * q8[j];
-        }
-      }
+    if (m < M) {
+      const int pq = a.P * a.Q;
+      const int n = m / pq;
+      const int rem = m - n * pq;
+      const int p = rem / a.Q;
+      const int q = rem - p * a.Q;
+      bh[i] = p * a.stride - a.pad_h;
+      bw[i] = q * a.stride - a.pad_w;
+      boff[i] = ((n * a.H + bh[i]) * a.W + bw[i]) * C + lc * 8;
+    } else {
+      bh[i] = -(1 << 28);
+      bw[i] = 0;
+      boff[i] = 0;
     }
   }
-  if (want_stats) {
-    __syncthreads();
-    float* red = tile;  // [256][16]
+  // wave-uniform k iterator of the next stage to issue: k offset, tap (r, s), channel offset
+  int ik = 0, ir = 0, is = 0, ici = 0;
+
+  auto issue = [&](int slot) {
+    char* st = smem + slot * STAGE;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      red[tid * 16 + j] = ssum[j];
-      red[tid * 16 + 8 + j] = ssq[j];
+    for (int i = 0; i < GA; ++i) {
+      const void* src = wsrc[i] ? (const void*)(wsrc[i] + ik) : zero;
+      glds16(src, st + (32 * i + 8 * wave) * ROWB);
     }
-    __syncthreads();
-    if (tid < 2 * BC) {
-      const int cl = tid >> 1, which = tid & 1;
-      const int chh = cl >> 3, j = cl & 7;
-      float s = 0.f;
-      for (int t2 = chh; t2 < 256; t2 += CHR) s += red[t2 * 16 + which * 8 + j];
-      if (c0 + cl < a.K) atomicAdd(a.stats + (size_t)which * a.K + c0 + cl, s);
+    const int tap_off = (ir * a.W + is) * C + ici;
+#pragma unroll
+    for (int i = 0; i < GB; ++i) {
+      const int h = bh[i] + ir, w = bw[i] + is;
+      const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+      const void* src = ok ? (const void*)(xg + (boff[i] + tap_off)) : zero;
+      glds16(src, st + (BC + 32 * i + 8 * wave) * ROWB);
     }
+    ik += 64;
+    ici += 64;
+    if (ici == C) {
+      ici = 0;
+      if (++is == a.S) {
+        is = 0;
+        ++ir;
+      }
+    }
+  };
+
+  const int wp = wave % WAVES_P;
+  const int wc = wave / WAVES_P;
+  f32x4_t acc[MI][MJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets (bytes, within a stage): row r, logical chunk kc -> slot kc ^ ((r>>1)&7)
+  const int fr = lane & 15, fk = lane >> 4;
+  int aoff[MI], boffl[MJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) aoff[i] = (wc * WC + i * 16 + fr) * ROWB;
+#pragma unroll
+  for (int j = 0; j < MJ; ++j) boffl[j] = (BC + wp * WP + j * 16 + fr) * ROWB;
+  const int swz = (fr >> 1) & 7;  // rows of a fragment group are 16-aligned: bits 1..3 = fr's
+
+  const int T = Ktot / 64;
+#pragma unroll
+  for (int s = 0; s < D; ++s)
+    if (s < T) issue(s);
+
+  for (int t = 0; t < T; ++t) {
+    // retire stage t: the stages issued after it (up to D-1) may stay in flight
+    if (t + D - 1 < T) wait_vmcnt<G * (D - 1)>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + D < T) issue((t + D) % NS);
+    const char* st = smem + (t % NS) * STAGE;
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh) {
+      const int slot = ((kh * 4 + fk) ^ swz) * 16;
+      bf16x8_t af[MI], bfr[MJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(st + aoff[i] + slot);
+#pragma unroll
+      for (int j = 0; j < MJ; ++j) bfr[j] = *reinterpret_cast<const bf16x8_t*>(st + boffl[j] + slot);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < MJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("" ::: "memory");
   }
+  __syncthreads();  // all fragment reads done before the epilogue reuses the LDS
+  static_assert(BP * BC * 4 <= NS * STAGE, "epilogue tile must fit the staging LDS");
+  conv_epilogue<BP, BC, WP, WC, MI, MJ>(a, smem, acc, wp, wc, m0, c0, M);
+}
+
+template <int BP, int BC, int WAVES_P, int NS>
+static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
+  constexpr int LDS = NS * (BC + BP) * 128;
+  static bool attr_set = false;
+  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS>;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr_set = true;
+  }
+  const int M = a->N * a->P * a->Q;
+  const int tiles_p = (M + BP - 1) / BP;
+  const int tiles_c = (a->K + BC - 1) / BC;
+  a->tiles_p = tiles_p;
+  hipLaunchKernelGGL(kern, dim3(tiles_p * tiles_c), dim3(256), LDS, stream, *a, zero);
+  return (int)hipGetLastError();
+}
+
+// Tile configurations of the LDS-DMA kernel (index = DRN conv config id, also used by the
+// host-side autotuner): {BP, BC, WAVES_P, NS}.
+#define DRN_GLDS_CONFIGS(X)  \
+  X(0, 128, 128, 2, 2)       \
+  X(1, 128, 128, 2, 3)       \
+  X(2, 128, 128, 2, 4)       \
+  X(3, 256, 64, 4, 2)        \
+  X(4, 256, 64, 4, 3)        \
+  X(5, 128, 64, 2, 3)        \
+  X(6, 64, 128, 1, 3)        \
+  X(7, 64, 64, 2, 4)
+
+static int launch_glds_cfg(int cfg, DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
+  switch (cfg) {
+#define DRN_X(id, bp, bc, wpv, ns) \
+  case id:                         \
+    return launch_conv_glds<bp, bc, wpv, ns>(a, zero, s);
+    DRN_GLDS_CONFIGS(DRN_X)
+#undef DRN_X
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+}
+
+static int glds_cfg_bp(int cfg) {
+  switch (cfg) {
+#define DRN_X(id, bp, bc, wpv, ns) \
+  case id:                         \
+    return bp;
+    DRN_GLDS_CONFIGS(DRN_X)
+#undef DRN_X
+    default:
+      return 0;
+  }
+}
+
+// Default choice when the host did not autotune (measured on the ResNet-50 layer set): the
+// 2-stage pipelines keep 2 blocks per CU resident, which beat deeper single-block pipelines;
+// 64 x 128 tiles once the 128 x 128 grid stops filling the chip.
+static int glds_default_cfg(const DrnConvFwdArgs* a) {
+  const long M = (long)a->N * a->P * a->Q;
+  auto blocks = [&](int bp, int bc) { return ((M + bp - 1) / bp) * ((a->K + bc - 1) / bc); };
+  if (a->K <= 64) return blocks(256, 64) >= 384 ? 3 : 7;
+  if (blocks(128, 128) >= 384) return 0;
+  return 6;
 }
 
 template <int BP, int BC, int BK, int WP, int WC, bool PRO, bool DIL2>
@@ -345,6 +586,25 @@ DRN_API int drn_conv_fwd_tiles_p(int M, int K) {
   const int BP = (K >= 128) ? 128 : 256;
   return (M + BP - 1) / BP;
 }
+
+DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s);
+
+// Whether the LDS-DMA kernel family supports this convolution.
+DRN_API int drn_conv_glds_ok(const DrnConvFwdArgs* a) {
+  return a->C % 64 == 0 && a->dil == 1 && a->in_scale == nullptr;
+}
+
+// Dispatch on a->cfg; zero = >= 16 bytes of device zeros (the LDS-DMA loader's padding source).
+DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
+  if ((a->C % 8) != 0 || (a->K % 8) != 0) return (int)hipErrorInvalidValue;
+  if (drn_conv_glds_ok(a) && zero != nullptr && a->cfg != 100)
+    return drn::launch_glds_cfg(a->cfg >= 0 ? a->cfg : drn::glds_default_cfg(a), a, zero, s);
+  return drn_conv_fwd(a, s);
+}
+
+DRN_API int drn_conv_glds_cfg_bp(int cfg) { return drn::glds_cfg_bp(cfg); }
+DRN_API int drn_conv_glds_num_cfgs() { return 8; }
+DRN_API int drn_conv_glds_default_cfg(const DrnConvFwdArgs* a) { return drn::glds_default_cfg(a); }
 
 DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s) {
   if ((a->C % 8) != 0 || (a->K % 8) != 0) return (int)hipErrorInvalidValue;

@@ -44,7 +44,7 @@ class DrnConvFwdArgs(ctypes.Structure):
         ("P", c_int), ("Q", c_int), ("stride", c_int), ("pad_h", c_int), ("pad_w", c_int), ("dil", c_int),
         ("relu_in", c_int), ("tiles_p", c_int),
         ("out_H", c_int), ("out_W", c_int), ("out_stride", c_int), ("out_oh", c_int), ("out_ow", c_int),
-        ("pad_", c_int),
+        ("cfg", c_int),
     ]
 
 
@@ -61,6 +61,10 @@ _SIGS = {
     "drn_version": ([], c_int),
     "drn_conv_fwd": ([ctypes.POINTER(DrnConvFwdArgs), c_p], c_int),
     "drn_conv_fwd_tiles_p": ([c_int, c_int], c_int),
+    "drn_conv_fwd2": ([ctypes.POINTER(DrnConvFwdArgs), c_p, c_p], c_int),
+    "drn_conv_glds_ok": ([ctypes.POINTER(DrnConvFwdArgs)], c_int),
+    "drn_conv_glds_num_cfgs": ([], c_int),
+    "drn_conv_glds_default_cfg": ([ctypes.POINTER(DrnConvFwdArgs)], c_int),
     "drn_conv_wgrad": ([ctypes.POINTER(DrnConvWgradArgs), c_p], c_int),
     "drn_splitk_reduce": ([c_p, c_p, c_i64, c_int, c_f, c_int, c_p], c_int),
     "drn_bn_stats": ([c_p, c_p, c_int, c_int, c_int, c_p], c_int),

@@ -18,6 +18,7 @@ where pre(x) = relu(x * scale + shift) when in_bn = (scale, shift) is given.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -104,6 +105,14 @@ class HipBackend(_Common):
     def __init__(self, device="cuda"):
         self.device = torch.device(device)
         self.L = _lib.lib()
+        # 4 KiB of device zeros: the padding source of the LDS-DMA conv loader
+        self.zero_page = torch.zeros(1024, dtype=torch.float32, device=self.device)
+        # conv kernel config per geometry key (set by the autotuner; -1 = library default)
+        self.conv_cfg: dict = {}
+        forced = os.environ.get("DRN_CONV_CFG")
+        self.forced_cfg = int(forced) if forced not in (None, "") else None
+        self.autotune = os.environ.get("DRN_AUTOTUNE", "1") == "1"
+        self.tune_log: list = []
 
     def stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -131,10 +140,58 @@ class HipBackend(_Common):
             a.out_H, a.out_W, a.out_stride, a.out_oh, a.out_ow = oH, oW, out_map.stride, out_map.oh, out_map.ow
         if stats is not None:
             assert stats.numel() >= 2 * K and stats.dtype == torch.float32, "stats accumulator must be fp32 [2][K]"
+        a.cfg = self.forced_cfg if self.forced_cfg is not None else self.conv_cfg.get(self.conv_key(a), -1)
         return a
 
+    @staticmethod
+    def conv_key(a) -> tuple:
+        return (a.N, a.H, a.W, a.C, a.K, a.R, a.S, a.P, a.Q, a.stride, a.pad_h, a.pad_w, a.dil,
+                a.in_scale is not None, a.out_stride)
+
     def launch_conv(self, a):
-        _lib.check(self.L.drn_conv_fwd(ctypes.byref(a), self.stream()), "drn_conv_fwd")
+        if a.cfg == -1 and self.autotune and self.forced_cfg is None:
+            key = self.conv_key(a)
+            if key not in self.conv_cfg and not torch.cuda.is_current_stream_capturing():
+                self.conv_cfg[key] = self._tune_conv(a, key)
+            a.cfg = self.conv_cfg.get(key, -1)
+        _lib.check(self.L.drn_conv_fwd2(ctypes.byref(a), self.zero_page.data_ptr(), self.stream()), "drn_conv_fwd")
+
+    def _tune_conv(self, a, key, iters: int = 5) -> int:
+        """Time every kernel configuration for this geometry (the MIOpen 'find' step, done once
+        per distinct convolution before the step is captured) and return the fastest. Runs on
+        scratch outputs / statistics so no live buffer is modified. Every configuration
+        accumulates each output in the same k order, so the choice does not change numerics."""
+        if not self.L.drn_conv_glds_ok(ctypes.byref(a)):
+            return 100
+        N, K = a.N, a.K
+        oh = a.out_H if a.out_stride else a.P
+        ow = a.out_W if a.out_stride else a.Q
+        y = torch.empty(N * oh * ow * K, dtype=torch.bfloat16, device=self.device)
+        st = torch.zeros(2 * K, dtype=torch.float32, device=self.device)
+        t = _lib.DrnConvFwdArgs()
+        ctypes.memmove(ctypes.addressof(t), ctypes.addressof(a), ctypes.sizeof(a))
+        t.y = y.data_ptr()
+        if a.residual is not None and a.residual == a.y:
+            t.residual = None
+        if a.stats is not None:
+            t.stats = st.data_ptr()
+        best, best_t = 100, float("inf")
+        s = self.stream()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for cfg in [100] + list(range(self.L.drn_conv_glds_num_cfgs())):
+            t.cfg = cfg
+            for _ in range(2):
+                _lib.check(self.L.drn_conv_fwd2(ctypes.byref(t), self.zero_page.data_ptr(), s), "drn_conv_fwd")
+            ev0.record()
+            for _ in range(iters):
+                _lib.check(self.L.drn_conv_fwd2(ctypes.byref(t), self.zero_page.data_ptr(), s), "drn_conv_fwd")
+            ev1.record()
+            ev1.synchronize()
+            ms = ev0.elapsed_time(ev1) / iters
+            if ms < best_t:
+                best, best_t = cfg, ms
+        self.tune_log.append((key, best, round(best_t * 1e3, 1)))
+        return best
 
     def conv_fwd(self, x, w, y, g, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None):
         self.launch_conv(self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats, out_map))

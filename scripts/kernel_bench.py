@@ -41,6 +41,9 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--json", default="")
     ap.add_argument("--only", default="", help="substring filter on the layer name (e.g. 'conv 256->256 k3s1')")
+    ap.add_argument("--pro", action="store_true", help="fused BN prologue in fwd/wgrad (default: materialized)")
+    ap.add_argument("--sweep", action="store_true", help="time every conv kernel config for fwd and dgrad")
+    ap.add_argument("--no_bn", action="store_true")
     a = ap.parse_args()
     spec = build_spec(a.dataset, a.resnet_size)
     be = HipBackend()
@@ -75,11 +78,26 @@ def main():
         st = torch.zeros(2, cout, device="cuda")
         dw = torch.empty(cout, k, k, cin, device="cuda")
         ws = torch.empty(max(16, be.wgrad_ws_elems(N * P * P, cout, k, k, cin)), device="cuda")
-        pro = None if kind == "stem" else (sc, sh)
+        pro = (sc, sh) if (a.pro and kind != "stem") else None
         flops = 2.0 * N * P * P * cout * k * k * cin
         t_f = timeit(lambda: be.conv_fwd(x, w, y, g, in_bn=pro, stats=st), a.iters)
         t_w = timeit(lambda: be.conv_wgrad(x, dy, dw, g, in_bn=pro, ws=ws), a.iters)
         t_d = timeit(lambda: be.conv_fwd(dy, wt, dx, dgrad_geom(g, k, k)), a.iters) if kind != "stem" else 0.0
+        if a.sweep:
+            from distributed_resnet_tensorflow_amd.ops.backend import dgrad_geom as _dg
+            res_f, res_d = [], []
+            for cfg in [100] + list(range(8)):
+                af = be.conv_args(x, w, y, g, in_bn=pro, stats=st)
+                af.cfg = cfg
+                res_f.append((timeit(lambda: be.launch_conv(af), a.iters), cfg))
+                if kind != "stem" and s == 1:
+                    ad = be.conv_args(dy, wt, dx, _dg(g, k, k))
+                    ad.cfg = cfg
+                    res_d.append((timeit(lambda: be.launch_conv(ad), a.iters), cfg))
+            fmt = lambda r: " ".join(f"{c}:{t:.0f}" for t, c in r)
+            print(f"sweep {kind} {cin}->{cout} k{k}s{s} @{H} x{cnt}: fwd best {min(res_f)} | {fmt(res_f)}", flush=True)
+            if res_d:
+                print(f"      dgrad best {min(res_d)} | {fmt(res_d)}", flush=True)
         bx, by = x.numel() * 2, y.numel() * 2
         r = dict(kind=kind, cin=cin, cout=cout, k=k, s=s, H=H, count=cnt,
                  fwd_us=t_f, fwd_tf=flops / t_f / 1e6, fwd_gbs=(bx + by) / t_f / 1e3,
@@ -99,7 +117,7 @@ def main():
               f"{r['wgrad_gbs']:6.0f}")
     print("totals per step (us):", {k: round(v, 1) for k, v in tot.items()})
     # BN backward kernels on the largest activation shapes
-    for (C, H) in ((64, 56), (256, 56), (128, 28), (512, 28), (1024, 14), (2048, 7)):
+    for (C, H) in (() if a.no_bn else ((64, 56), (256, 56), (128, 28), (512, 28), (1024, 14), (2048, 7))):
         x = torch.randn(N, H, H, C, device="cuda").bfloat16()
         da = torch.randn_like(x)
         out = torch.empty_like(x)

@@ -7,7 +7,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from distributed_resnet_tensorflow_amd.ops.backend import ConvGeom, dgrad_geom, tflip_desc, tflip_table
+from distributed_resnet_tensorflow_amd.ops.backend import OutMap, ConvGeom, dgrad_geom, tflip_desc, tflip_table
 
 pytestmark = pytest.mark.gpu
 
@@ -69,6 +69,62 @@ def test_conv_fwd(hip, ref, case, fused):
     s_hip = st.view(-1).cpu()
     assert rel(s_hip[:K], st_ref[:K]) < 2e-2
     assert rel(s_hip[K:], st_ref[K:]) < 2e-2
+
+
+GLDS_CASES = [
+    # N, H, W, C, K, R, stride, pad   (C % 64 == 0: LDS-DMA kernel family)
+    (2, 9, 9, 64, 64, 3, 1, 1),        # M=162: partial pixel tiles for every BP
+    (3, 7, 7, 128, 256, 1, 1, 0),
+    (2, 13, 13, 64, 128, 3, 2, 1),     # stride 2, odd size, padding
+    (1, 6, 6, 192, 72, 3, 1, 1),       # K % BC != 0 (zero-page weight rows)
+    (2, 8, 8, 256, 64, 1, 2, 0),
+]
+
+
+@pytest.mark.parametrize("case", GLDS_CASES)
+@pytest.mark.parametrize("cfg", list(range(8)))
+def test_conv_fwd_glds_configs(hip, ref, case, cfg):
+    """Every tile/pipeline configuration of the LDS-DMA conv kernel vs the fp32 reference,
+    with residual add + BN statistics epilogue."""
+    N, H, W, C, K, R, s, p = case
+    torch.manual_seed(10 + cfg)
+    P = out_size(H, R, s, p)
+    x = bf(torch.randn(N, H, W, C))
+    w = bf(torch.randn(K, R, R, C) * (2.0 / (R * R * C)) ** 0.5)
+    res = bf(torch.randn(N, P, P, K))
+    g = ConvGeom(stride=s, pad_h=p, pad_w=p)
+    y_ref = torch.zeros(N, P, P, K)
+    st_ref = torch.zeros(2 * K)
+    ref.conv_fwd(x.float(), w.float(), y_ref, g, residual=res.float(), stats=st_ref)
+    y = torch.zeros(N, P, P, K, dtype=torch.bfloat16, device="cuda")
+    st = torch.zeros(2, K, device="cuda")
+    a = hip.conv_args(x.cuda(), w.cuda(), y, g, residual=res.cuda(), stats=st)
+    assert hip.L.drn_conv_glds_ok(a) == 1
+    a.cfg = cfg
+    hip.launch_conv(a)
+    torch.cuda.synchronize()
+    assert rel(y, y_ref) < 1e-2
+    s_hip = st.view(-1).cpu()
+    assert rel(s_hip[:K], st_ref[:K]) < 2e-2
+    assert rel(s_hip[K:], st_ref[K:]) < 2e-2
+
+
+def test_conv_glds_out_map(hip, ref):
+    """Phase output mapping (stride-2 data-gradient phases) through the LDS-DMA kernel."""
+    torch.manual_seed(5)
+    N, P, C, K = 2, 5, 64, 64
+    x = bf(torch.randn(N, P, P, C))
+    w = bf(torch.randn(K, 1, 1, C) * 0.1)
+    om = OutMap(P=P, Q=P, stride=2, oh=1, ow=0)
+    y_ref = torch.zeros(N, 2 * P, 2 * P, K)
+    ref.conv_fwd(x.float(), w.float(), y_ref, ConvGeom(1, 0, 0), out_map=om)
+    for cfg in range(8):
+        y = torch.zeros(N, 2 * P, 2 * P, K, dtype=torch.bfloat16, device="cuda")
+        a = hip.conv_args(x.cuda(), w.cuda(), y, ConvGeom(1, 0, 0), out_map=om)
+        a.cfg = cfg
+        hip.launch_conv(a)
+        torch.cuda.synchronize()
+        assert rel(y, y_ref) < 1e-2, cfg
 
 
 @pytest.mark.parametrize("case", CONV_CASES[:-1])
