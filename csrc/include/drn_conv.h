@@ -36,6 +36,15 @@ struct DrnConvFwdArgs {
   // Kernel configuration for drn_conv_fwd2: -1 automatic, 0..7 an LDS-DMA tile configuration
   // (DRN_GLDS_CONFIGS), 100 the register-staged kernel.
   int32_t cfg;
+  // Optional fused BatchNorm-backward reduction (data-gradient launches): when bn_x is set the
+  // conv output v is d/d relu(bn(bn_x)); the epilogue stores the ReLU-masked gradient
+  // g = v * [bn_x*scale+shift > 0] and accumulates stats[0][k] += g,
+  // stats[1][k] += g * (bn_x - mean) * invstd instead of the forward statistics.
+  const void* bn_x;       // bf16, same layout as y
+  const float* bn_scale;
+  const float* bn_shift;
+  const float* bn_mean;
+  const float* bn_invstd;
 };
 
 // dW[K][R][S][C] (+)= sum_{n,p,q} dy[n,p,q,k] * x[n, p*st-pad+r, q*st-pad+s, c]

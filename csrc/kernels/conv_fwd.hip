@@ -26,19 +26,65 @@
 namespace drn {
 
 // ---------------- shared epilogue ----------------
+// Every lane owns 8 consecutive channels (one 16-byte bf16 chunk) of BP/RPI pixel rows.
+// epi_prefetch() computes those output offsets and issues the 16-byte loads of the residual
+// and of the fused-BN-backward input BEFORE the main loop, so their latency hides behind the
+// MFMA work instead of stalling the epilogue (short-K launches are otherwise dominated by it).
+template <int BP, int BC>
+struct EpiPre {
+  static constexpr int CHR = BC / 8;  // output 16-byte chunks per pixel row
+  static constexpr int RPI = 256 / CHR;
+  static constexpr int IT = BP / RPI;
+  int off[IT];     // element offset of the chunk, -1 when outside the output
+  uint4 res[IT];
+  uint4 bx[IT];
+};
+
+template <int BP, int BC>
+__device__ __forceinline__ void epi_prefetch(const DrnConvFwdArgs& a, int m0, int c0, int M, EpiPre<BP, BC>& e) {
+  using E = EpiPre<BP, BC>;
+  const int tid = threadIdx.x;
+  const int ch = tid % E::CHR;
+  const int c = c0 + ch * 8;
+  const bool mapped = a.out_stride != 0;
+  const int pq = a.P * a.Q;
+  const bf16_t* __restrict__ res = reinterpret_cast<const bf16_t*>(a.residual);
+  const bf16_t* __restrict__ bx = reinterpret_cast<const bf16_t*>(a.bn_x);
+#pragma unroll
+  for (int it = 0; it < E::IT; ++it) {
+    const int m = m0 + it * E::RPI + tid / E::CHR;
+    int off = -1;
+    if (m < M && c < a.K) {
+      if (mapped) {
+        const int n = m / pq;
+        const int rem = m - n * pq;
+        const int i = rem / a.Q;
+        const int j = rem - i * a.Q;
+        off = ((n * a.out_H + i * a.out_stride + a.out_oh) * a.out_W + j * a.out_stride + a.out_ow) * a.K + c;
+      } else {
+        off = m * a.K + c;
+      }
+    }
+    e.off[it] = off;
+    e.res[it] = (res && off >= 0) ? *reinterpret_cast<const uint4*>(res + off) : make_uint4(0u, 0u, 0u, 0u);
+    e.bx[it] = (bx && off >= 0) ? *reinterpret_cast<const uint4*>(bx + off) : make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
 // The fp32 accumulator tile is staged through LDS ([BP][BC] fp32, 16-byte chunks XOR-swizzled
 // by row: conflict-free 8-lane ds_write_b128 groups and 16-lane ds_read_b128 groups), then
-// every lane owns 8 consecutive channels of one pixel: 16-byte residual loads and 16-byte
-// bf16 stores, whole 2*BC-byte pixel rows per wave instruction (fully coalesced). Optional
-// residual add, optional strided output map, optional per-channel sum/sumsq for the next BN.
+// written as whole 2*BC-byte pixel rows per wave instruction (fully coalesced). Optional
+// residual add, optional strided output map, optional per-channel sum/sumsq for the next BN,
+// or (bn_x set) the fused BN-backward reduction with ReLU-masked output.
 template <int BP, int BC, int WP, int WC, int MI, int MJ>
 __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* smem, f32x4_t (&acc)[MI][MJ], int wp,
-                                              int wc, int m0, int c0, int M) {
+                                              int wc, int m0, int c0, int M, const EpiPre<BP, BC>& e) {
+  using E = EpiPre<BP, BC>;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   constexpr int CF = BC / 4;   // fp32 16-byte chunks per staged row
-  constexpr int CHR = BC / 8;  // output 16-byte (8 x bf16) chunks per pixel row
-  constexpr int RPI = 256 / CHR;
+  constexpr int CHR = E::CHR;
+  constexpr int RPI = E::RPI;
   constexpr int SWM = CF >= 8 ? 7 : CF - 1;  // swizzle mask stays inside a staged row
   float* tile = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -53,47 +99,60 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
   __syncthreads();
   const bool want_stats = a.stats != nullptr;
   bf16_t* __restrict__ y = reinterpret_cast<bf16_t*>(a.y);
-  const bf16_t* __restrict__ res = reinterpret_cast<const bf16_t*>(a.residual);
+  const bool has_res = a.residual != nullptr;
   const int ch = tid % CHR;
   const int c = c0 + ch * 8;
-  const bool mapped = a.out_stride != 0;
-  const int pq = a.P * a.Q;
+  const bool bnb = a.bn_x != nullptr;
   float ssum[8], ssq[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) ssum[j] = ssq[j] = 0.f;
+  float bsc[8], bsh[8], bmu[8], bis[8];
+  if (bnb && c < a.K) {
 #pragma unroll
-  for (int it = 0; it < BP / RPI; ++it) {
+    for (int j = 0; j < 8; ++j) {
+      bsc[j] = a.bn_scale[c + j];
+      bsh[j] = a.bn_shift[c + j];
+      bmu[j] = a.bn_mean[c + j];
+      bis[j] = a.bn_invstd[c + j];
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < E::IT; ++it) {
     const int row = it * RPI + tid / CHR;
-    const int m = m0 + row;
     const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(tile + row * BC + (((2 * ch) ^ (row & SWM)) * 4));
     const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(tile + row * BC + (((2 * ch + 1) ^ (row & SWM)) * 4));
-    if (m < M && c < a.K) {
+    const int off = e.off[it];
+    if (off >= 0) {
       float f[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      size_t off;
-      if (mapped) {
-        const int n = m / pq;
-        const int rem = m - n * pq;
-        const int i = rem / a.Q;
-        const int j = rem - i * a.Q;
-        off = ((size_t)(n * a.out_H + i * a.out_stride + a.out_oh) * a.out_W + j * a.out_stride + a.out_ow) * a.K + c;
-      } else {
-        off = (size_t)m * a.K + c;
-      }
-      if (res) {
+      if (has_res) {
         float r8[8];
-        unpack8(*reinterpret_cast<const uint4*>(res + off), r8);
+        unpack8(e.res[it], r8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] += r8[j];
       }
       const uint4 o = pack8(f);
-      *reinterpret_cast<uint4*>(y + off) = o;
-      if (want_stats) {
-        float q8[8];
-        unpack8(o, q8);
+      float q8[8];
+      unpack8(o, q8);
+      if (bnb) {
+        // BN-backward: mask by the forward ReLU, accumulate sum g and sum g * xhat
+        float xb[8];
+        unpack8(e.bx[it], xb);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          ssum[j] += q8[j];
-          ssq[j] += q8[j] * q8[j];
+          const float g = (xb[j] * bsc[j] + bsh[j] > 0.f) ? q8[j] : 0.f;
+          f[j] = g;
+          ssum[j] += g;
+          ssq[j] += g * ((xb[j] - bmu[j]) * bis[j]);
+        }
+        *reinterpret_cast<uint4*>(y + off) = pack8(f);
+      } else {
+        *reinterpret_cast<uint4*>(y + off) = o;
+        if (want_stats) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            ssum[j] += q8[j];
+            ssq[j] += q8[j] * q8[j];
+          }
         }
       }
     }
@@ -318,7 +377,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(DrnConvFwdArgs a) {
   }
 
   static_assert(BP * BC * 4 <= 2 * STAGE, "epilogue tile must fit the staging LDS");
-  conv_epilogue<BP, BC, WP, WC, MI, MJ>(a, smem, acc, wp, wc, m0, c0, M);
+  EpiPre<BP, BC> epre;
+  epi_prefetch<BP, BC>(a, m0, c0, M, epre);
+  conv_epilogue<BP, BC, WP, WC, MI, MJ>(a, smem, acc, wp, wc, m0, c0, M, epre);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -456,6 +517,8 @@ __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(DrnConvFwdArgs a, co
   const int swz = (fr >> 1) & 7;  // rows of a fragment group are 16-aligned: bits 1..3 = fr's
 
   const int T = Ktot / 64;
+  EpiPre<BP, BC> epre;
+  epi_prefetch<BP, BC>(a, m0, c0, M, epre);  // residual / BN inputs in flight during the main loop
 #pragma unroll
   for (int s = 0; s < D; ++s)
     if (s < T) issue(s);
@@ -486,7 +549,7 @@ __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(DrnConvFwdArgs a, co
   }
   __syncthreads();  // all fragment reads done before the epilogue reuses the LDS
   static_assert(BP * BC * 4 <= NS * STAGE, "epilogue tile must fit the staging LDS");
-  conv_epilogue<BP, BC, WP, WC, MI, MJ>(a, smem, acc, wp, wc, m0, c0, M);
+  conv_epilogue<BP, BC, WP, WC, MI, MJ>(a, smem, acc, wp, wc, m0, c0, M, epre);
 }
 
 template <int BP, int BC, int WAVES_P, int NS>

@@ -258,6 +258,281 @@ static int dispatch_wgrad(DrnConvWgradArgs* a, hipStream_t s) {
   return launch_wgrad<64, 64, PRO>(a, s);
 }
 
+// ---------------------------------------------------------------------------------------
+// LDS-DMA variant (no fused prologue): both operand images are filled by
+// `global_load_lds_dwordx4` NS stages deep (counted vmcnt + raw barrier, like the forward
+// kernel), so the 64-pixel steps no longer wait on a register round trip. The images keep the
+// exact swizzled layout the transposed reads above expect; an LDS-DMA writes lane-linear, so
+// the 32-byte-slot swizzle is applied to the per-lane SOURCE address instead: lane i of a
+// wave-instruction fills physical 16-byte chunk (i mod W/16) of row (i div W/16) and therefore
+// loads logical chunk 2*(slot ^ h(row)) + half. With wave w issuing instructions w, w+4, ...
+// the swizzle bit that varies between instructions is wave-uniform, so each lane decodes its
+// (tap, channel) chunk once. Out-of-image taps, pixels past the split and channels past K
+// read the zero page.
+// ---------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void wg_lds_void;
+typedef __attribute__((address_space(1))) const void wg_gbl_void;
+
+template <int N>
+__device__ __forceinline__ void wg_wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int V>
+struct drn_int_c {
+  static constexpr int value = V;
+};
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(drn_int_c<B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+template <int OFF>
+__device__ __forceinline__ s16x4v tr_read_asm(uint32_t addr) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
+  s16x4v r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+
+// s_waitcnt lgkmcnt(N) that the fragments it retires depend on (so no MFMA reading them can be
+// scheduled above it).
+template <int N, int MI, int MJ>
+__device__ __forceinline__ void lgkm_fence(s16x4v (&a)[MI][2], s16x4v (&b)[MJ][2]) {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+#pragma unroll
+  for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(a[i][0]), "+v"(a[i][1]));
+#pragma unroll
+  for (int j = 0; j < MJ; ++j) asm volatile("" : "+v"(b[j][0]), "+v"(b[j][1]));
+}
+
+template <int BKK, int BCO, int NS>
+__global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a, const void* __restrict__ zero) {
+  constexpr int BP = 64;
+  constexpr int WA = BKK * 2, WB = BCO * 2;       // image row bytes
+  constexpr int A_BYTES = BP * WA;
+  constexpr int STAGE = A_BYTES + BP * WB;
+  constexpr int LPA = WA / 16, LPB = WB / 16;     // lanes per row in one wave-instruction
+  constexpr int RIA = 64 / LPA, RIB = 64 / LPB;   // rows per wave-instruction
+  constexpr int IA = BP / RIA / 4, IB = BP / RIB / 4;  // instructions per wave per stage
+  constexpr int G = IA + IB;
+  constexpr int D = NS - 1;
+  constexpr int WKK = BKK / 2, WCO = BCO / 2;
+  constexpr int MI = WKK / 16, MJ = WCO / 16;
+  static_assert(IA >= 1 && IB >= 1 && NS >= 2, "geometry");
+
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int Ktot = a.R * a.S * a.C;
+  const int M = a.N * a.P * a.Q;
+  const int nkt = (Ktot + BKK - 1) / BKK;
+  const int kt = blockIdx.x % nkt;
+  const int ct = blockIdx.x / nkt;
+  const int k0 = kt * BKK, c0 = ct * BCO;
+  const int split = blockIdx.y;
+  const int mbeg = split * a.pix_per_split;
+  const int mend = min(M, mbeg + a.pix_per_split);
+
+  // ---- A (patches) loader: row-in-instruction and logical chunk of this lane ----
+  const int arow = lane / LPA;                 // + RIA * instruction
+  int alc;
+  {
+    const int pc = lane % LPA;
+    // row of the first instruction of this wave; the swizzle of later ones is identical
+    const int row = RIA * wave + arow;
+    alc = 2 * ((pc >> 1) ^ slot_swz<WA>(row)) + (pc & 1);
+  }
+  const int kk = k0 + alc * 8;
+  const bool kvalid = kk < Ktot;
+  int ci = 0, rr = 0, ss = 0;
+  if (kvalid) {
+    const int tap = kk / a.C;
+    ci = kk - tap * a.C;
+    rr = tap / a.S;
+    ss = tap - rr * a.S;
+  }
+  const int roff = rr - a.pad_h, soff = ss - a.pad_w;
+  // ---- B (dY) loader ----
+  const int brow = lane / LPB;
+  int blc;
+  {
+    const int pc = lane % LPB;
+    const int row = RIB * wave + brow;
+    blc = 2 * ((pc >> 1) ^ slot_swz<WB>(row)) + (pc & 1);
+  }
+  const int dc = c0 + blc * 8;
+  const bool cvalid = dc < a.K;
+  const bf16_t* __restrict__ xg = reinterpret_cast<const bf16_t*>(a.x);
+  const bf16_t* __restrict__ dyg = reinterpret_cast<const bf16_t*>(a.dy) + dc;
+  // Pixel coordinates of this lane's A rows, decoded once and then advanced by 64 pixels per
+  // stage with adds/compares (a magic-number division per row per stage made the loader
+  // VALU-bound: mul_hi/mul_lo/64-bit mads are quarter rate). Offsets use 24-bit multiplies
+  // (every ResNet activation dimension product is < 2^24).
+  const int HWC = a.H * a.W * a.C, WC = a.W * a.C;
+  const int dq = BP % a.Q, dp = BP / a.Q;
+  int am[IA], an[IA], ap[IA], aq[IA];
+#pragma unroll
+  for (int i = 0; i < IA; ++i) {
+    const int m = mbeg + RIA * (wave + 4 * i) + arow;
+    am[i] = m;
+    const uint32_t n = fdiv((uint32_t)m, a.fd_pq);
+    const uint32_t rem = (uint32_t)m - n * (uint32_t)(a.P * a.Q);
+    const uint32_t p = fdiv(rem, a.fd_q);
+    an[i] = (int)n;
+    ap[i] = (int)p;
+    aq[i] = (int)(rem - p * (uint32_t)a.Q);
+  }
+
+  auto issue = [&](int slot, int mstep) {
+    char* st = smem + slot * STAGE;
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      const int r0 = RIA * (wave + 4 * i);
+      const int h = __mul24(ap[i], a.stride) + roff;
+      const int w = __mul24(aq[i], a.stride) + soff;
+      const bool ok = kvalid && am[i] < mend && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+      const uint32_t off = (uint32_t)(__mul24(an[i], HWC) + __mul24(h, WC) + __mul24(w, a.C) + ci);
+      const void* src = ok ? (const void*)(xg + off) : zero;
+      __builtin_amdgcn_global_load_lds((wg_gbl_void*)src, (wg_lds_void*)(st + r0 * WA), 16, 0, 0);
+      am[i] += BP;
+      aq[i] += dq;
+      ap[i] += dp;
+      if (aq[i] >= a.Q) {
+        aq[i] -= a.Q;
+        ++ap[i];
+      }
+      while (ap[i] >= a.P) {
+        ap[i] -= a.P;
+        ++an[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int r0 = RIB * (wave + 4 * i);
+      const int m = mstep + r0 + brow;
+      const void* src = (cvalid && m < mend) ? (const void*)(dyg + (uint32_t)__mul24(m, a.K)) : zero;
+      __builtin_amdgcn_global_load_lds((wg_gbl_void*)src, (wg_lds_void*)(st + A_BYTES + r0 * WB), 16, 0, 0);
+    }
+  };
+
+  f32x4_t acc[MI][MJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int T = (mend > mbeg) ? (mend - mbeg + BP - 1) / BP : 0;
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  const int wk = wave & 1, wc = wave >> 1;
+  const uint32_t lds_base = (uint32_t)reinterpret_cast<uintptr_t>(smem);  // LDS offset of the image
+  // Fragment addresses: swz_off(32ks + 4hi + 8g + q4, col) = swz_off(8g + q4, col) + (32ks + 4hi) * W,
+  // because the row swizzle only looks at row bits 0,1,3 (unchanged by +4 and +32): the
+  // k-slice / half part is an immediate offset of the read.
+  uint32_t a_lane[MI], b_lane[MJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) a_lane[i] = (uint32_t)swz_off<WA>(8 * g + q4, wk * WKK + 16 * i + 4 * p4);
+#pragma unroll
+  for (int j = 0; j < MJ; ++j) b_lane[j] = (uint32_t)swz_off<WB>(8 * g + q4, wc * WCO + 16 * j + 4 * p4);
+
+#pragma unroll
+  for (int s = 0; s < D; ++s)
+    if (s < T) issue(s, mbeg + s * BP);
+
+  for (int t = 0; t < T; ++t) {
+    if (t + D - 1 < T) wg_wait_vmcnt<G * (D - 1)>();
+    else wg_wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + D < T) issue((t + D) % NS, mbeg + (t + D) * BP);
+    // Transposed fragment reads in inline asm: hipcc treats its ds_read_tr intrinsic as
+    // possibly aliasing the LDS-DMA just issued and would wait vmcnt(0) (serialising the
+    // pipeline); the asm reads are ordered by hand instead: both k-slices' reads are issued,
+    // lgkmcnt(16) retires the first 16 (LDS returns in order), lgkmcnt(0) the rest.
+    const uint32_t cur = lds_base + (uint32_t)((t % NS) * STAGE);
+    uint32_t ba[MI], bb[MJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) ba[i] = cur + a_lane[i];
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) bb[j] = cur + b_lane[j];
+    s16x4v fa[2][MI][2], fb[2][MJ][2];
+    static_for<0, 2>([&](auto KS) {
+      constexpr int ks = decltype(KS)::value;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        fa[ks][i][0] = tr_read_asm<(32 * ks) * WA>(ba[i]);
+        fa[ks][i][1] = tr_read_asm<(32 * ks + 4) * WA>(ba[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < MJ; ++j) {
+        fb[ks][j][0] = tr_read_asm<A_BYTES + (32 * ks) * WB>(bb[j]);
+        fb[ks][j][1] = tr_read_asm<A_BYTES + (32 * ks + 4) * WB>(bb[j]);
+      }
+    });
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      if (ks == 0) lgkm_fence<(2 * (MI + MJ) > 15 ? 15 : 2 * (MI + MJ))>(fa[0], fb[0]);  // 4-bit counter
+      else lgkm_fence<0>(fa[1], fb[1]);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < MJ; ++j) {
+          const bf16x8_t af = __builtin_bit_cast(
+              bf16x8_t, __builtin_shufflevector(fa[ks][i][0], fa[ks][i][1], 0, 1, 2, 3, 4, 5, 6, 7));
+          const bf16x8_t bfr = __builtin_bit_cast(
+              bf16x8_t, __builtin_shufflevector(fb[ks][j][0], fb[ks][j][1], 0, 1, 2, 3, 4, 5, 6, 7));
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[i][j], 0, 0, 0);
+        }
+    }
+    asm volatile("" ::: "memory");
+  }
+
+  float* out = a.out + (size_t)split * a.K * Ktot;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) {
+      const int co = c0 + wc * WCO + 16 * j + (lane & 15);
+      const int kr = k0 + wk * WKK + 16 * i + 4 * (lane >> 4);
+      if (co < a.K && kr < Ktot) *reinterpret_cast<f32x4_t*>(out + (size_t)co * Ktot + kr) = acc[i][j];
+    }
+}
+
+template <int BKK, int BCO, int NS>
+static int launch_wgrad_glds(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
+  constexpr int LDS = NS * (64 * BKK * 2 + 64 * BCO * 2);
+  static bool attr_set = false;
+  auto kern = conv_wgrad_glds_kernel<BKK, BCO, NS>;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr_set = true;
+  }
+  const int Ktot = a->R * a->S * a->C;
+  const int nkt = (Ktot + BKK - 1) / BKK;
+  const int nct = (a->K + BCO - 1) / BCO;
+  hipLaunchKernelGGL(kern, dim3(nkt * nct, a->splits), dim3(256), LDS, s, *a, zero);
+  return (int)hipGetLastError();
+}
+
+static int dispatch_wgrad_glds(DrnConvWgradArgs* a, const void* zero, int ns, hipStream_t s) {
+  const int Ktot = a->R * a->S * a->C;
+  const bool wide_k = Ktot > 64;
+  const bool wide_c = a->K > 64;
+  if (ns == 3) {
+    if (wide_k && wide_c) return launch_wgrad_glds<128, 128, 3>(a, zero, s);
+    if (wide_k) return launch_wgrad_glds<128, 64, 3>(a, zero, s);
+    if (wide_c) return launch_wgrad_glds<64, 128, 3>(a, zero, s);
+    return launch_wgrad_glds<64, 64, 3>(a, zero, s);
+  }
+  if (wide_k && wide_c) return launch_wgrad_glds<128, 128, 2>(a, zero, s);
+  if (wide_k) return launch_wgrad_glds<128, 64, 2>(a, zero, s);
+  if (wide_c) return launch_wgrad_glds<64, 128, 2>(a, zero, s);
+  return launch_wgrad_glds<64, 64, 2>(a, zero, s);
+}
+
 // out[i] (+)= scale * sum_k ws[k][i]: block = 64 float4 columns x 4 split-groups; every
 // thread keeps 4 independent loads in flight (the split loop is the latency chain for small
 // tensors with many splits), then the 4 groups are summed through LDS in a fixed order
@@ -319,6 +594,14 @@ DRN_API int drn_conv_wgrad(DrnConvWgradArgs* a, hipStream_t s) {
   if ((a->C % 8) != 0 || (a->K % 8) != 0 || a->splits < 1 || (a->pix_per_split % 64) != 0)
     return (int)hipErrorInvalidValue;
   return a->in_scale != nullptr ? drn::dispatch_wgrad<true>(a, s) : drn::dispatch_wgrad<false>(a, s);
+}
+
+// LDS-DMA wgrad (no prologue); ns = pipeline stages (2 or 3), 0 = register-staged kernel.
+DRN_API int drn_conv_wgrad2(DrnConvWgradArgs* a, const void* zero, int ns, hipStream_t s) {
+  if ((a->C % 8) != 0 || (a->K % 8) != 0 || a->splits < 1 || (a->pix_per_split % 64) != 0)
+    return (int)hipErrorInvalidValue;
+  if (a->in_scale != nullptr || zero == nullptr || ns == 0) return drn_conv_wgrad(a, s);
+  return drn::dispatch_wgrad_glds(a, zero, ns, s);
 }
 
 // out[i] (+)= scale * sum_k ws[k][i]  over n floats (n % 4 == 0), deterministic order.

@@ -45,6 +45,7 @@ class DrnConvFwdArgs(ctypes.Structure):
         ("relu_in", c_int), ("tiles_p", c_int),
         ("out_H", c_int), ("out_W", c_int), ("out_stride", c_int), ("out_oh", c_int), ("out_ow", c_int),
         ("cfg", c_int),
+        ("bn_x", c_p), ("bn_scale", c_p), ("bn_shift", c_p), ("bn_mean", c_p), ("bn_invstd", c_p),
     ]
 
 
@@ -66,6 +67,7 @@ _SIGS = {
     "drn_conv_glds_num_cfgs": ([], c_int),
     "drn_conv_glds_default_cfg": ([ctypes.POINTER(DrnConvFwdArgs)], c_int),
     "drn_conv_wgrad": ([ctypes.POINTER(DrnConvWgradArgs), c_p], c_int),
+    "drn_conv_wgrad2": ([ctypes.POINTER(DrnConvWgradArgs), c_p, c_int, c_p], c_int),
     "drn_splitk_reduce": ([c_p, c_p, c_i64, c_int, c_f, c_int, c_p], c_int),
     "drn_bn_stats": ([c_p, c_p, c_int, c_int, c_int, c_p], c_int),
     "drn_bn_finalize": ([c_p, c_int, c_int, c_f, c_p, c_p, c_f, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_int),

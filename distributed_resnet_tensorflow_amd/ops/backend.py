@@ -112,13 +112,17 @@ class HipBackend(_Common):
         forced = os.environ.get("DRN_CONV_CFG")
         self.forced_cfg = int(forced) if forced not in (None, "") else None
         self.autotune = os.environ.get("DRN_AUTOTUNE", "1") == "1"
+        self.wgrad_ns: dict = {}
+        forced = os.environ.get("DRN_WGRAD_NS")
+        self.forced_wgrad_ns = int(forced) if forced not in (None, "") else None
         self.tune_log: list = []
 
     def stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream
 
     # -- conv ---------------------------------------------------------------------------------
-    def conv_args(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None):
+    def conv_args(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None,
+                  bn_bwd=None):
         N, H, W, C = x.shape
         K, R, S, C2 = w.shape
         N2, P, Q, K2 = y.shape
@@ -140,6 +144,12 @@ class HipBackend(_Common):
             a.out_H, a.out_W, a.out_stride, a.out_oh, a.out_ow = oH, oW, out_map.stride, out_map.oh, out_map.ow
         if stats is not None:
             assert stats.numel() >= 2 * K and stats.dtype == torch.float32, "stats accumulator must be fp32 [2][K]"
+        if bn_bwd is not None:
+            assert stats is not None, "fused BN-backward reduction accumulates into stats"
+            bx, bsc, bsh, bmu, bis = bn_bwd
+            assert bx.shape == y.shape
+            a.bn_x, a.bn_scale, a.bn_shift = bx.data_ptr(), bsc.data_ptr(), bsh.data_ptr()
+            a.bn_mean, a.bn_invstd = bmu.data_ptr(), bis.data_ptr()
         a.cfg = self.forced_cfg if self.forced_cfg is not None else self.conv_cfg.get(self.conv_key(a), -1)
         return a
 
@@ -193,8 +203,10 @@ class HipBackend(_Common):
         self.tune_log.append((key, best, round(best_t * 1e3, 1)))
         return best
 
-    def conv_fwd(self, x, w, y, g, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None):
-        self.launch_conv(self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats, out_map))
+    def conv_fwd(self, x, w, y, g, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None, bn_bwd=None):
+        """y = conv(x) (+ residual); optional BN statistics of y, or (bn_bwd = (x_bn, scale, shift,
+        mean, invstd)) the fused BN-backward reduction with ReLU-masked output."""
+        self.launch_conv(self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd))
 
     @staticmethod
     def wgrad_splits(M, Ktot, K, target_blocks: int = 640, min_steps: int = 8):
@@ -238,9 +250,46 @@ class HipBackend(_Common):
         splits, _ = self.wgrad_splits(M, R * S * C, K)
         return splits * K * R * S * C if splits > 1 else 0
 
+    @staticmethod
+    def wgrad_key(a) -> tuple:
+        return (a.N, a.H, a.W, a.C, a.K, a.R, a.S, a.P, a.Q, a.stride, a.pad_h, a.pad_w,
+                a.in_scale is not None, a.splits)
+
+    def _wgrad_kernel(self, a, ns: int, st):
+        _lib.check(self.L.drn_conv_wgrad2(ctypes.byref(a), self.zero_page.data_ptr(), ns, st), "drn_conv_wgrad")
+
+    def _tune_wgrad(self, a, key, iters: int = 5) -> int:
+        """Pick the wgrad pipeline (0: register-staged, 2/3: LDS-DMA stages) by timing; the
+        kernel only writes the split-K workspace (or the gradient slot, rewritten right after)."""
+        if a.in_scale is not None:
+            return 0
+        st = self.stream()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        best, best_t = 2, float("inf")
+        for ns in (0, 2, 3):
+            for _ in range(2):
+                self._wgrad_kernel(a, ns, st)
+            ev0.record()
+            for _ in range(iters):
+                self._wgrad_kernel(a, ns, st)
+            ev1.record()
+            ev1.synchronize()
+            ms = ev0.elapsed_time(ev1) / iters
+            if ms < best_t:
+                best, best_t = ns, ms
+        self.tune_log.append((("wgrad",) + key, best, round(best_t * 1e3, 1)))
+        return best
+
     def launch_wgrad(self, a, out):
         st = self.stream()
-        _lib.check(self.L.drn_conv_wgrad(ctypes.byref(a), st), "drn_conv_wgrad")
+        if self.forced_wgrad_ns is not None:
+            ns = self.forced_wgrad_ns
+        else:
+            key = self.wgrad_key(a)
+            if key not in self.wgrad_ns and self.autotune and not torch.cuda.is_current_stream_capturing():
+                self.wgrad_ns[key] = self._tune_wgrad(a, key)
+            ns = self.wgrad_ns.get(key, 2)
+        self._wgrad_kernel(a, ns, st)
         if a.splits > 1:
             _lib.check(self.L.drn_splitk_reduce(a.out, out.data_ptr(), out.numel(), a.splits, 1.0, 0, st),
                        "drn_splitk_reduce")
@@ -428,7 +477,8 @@ class RefBackend(_Common):
     def stream(self):
         return None
 
-    def conv_fwd(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None):
+    def conv_fwd(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None,
+                 bn_bwd=None):
         K, R, S, C = w.shape
         _, P, Q, _ = y.shape
         if out_map is not None:
@@ -436,17 +486,26 @@ class RefBackend(_Common):
         xc = _dilate(_pre(x, in_bn, relu_in).permute(0, 3, 1, 2), g.dil)
         xc = _pad_for(xc, P, Q, R, S, g)
         out = F.conv2d(xc, w.to(_DT[0]).permute(0, 3, 1, 2), stride=g.stride).permute(0, 2, 3, 1)
+        sl = None
         if out_map is not None:
             sl = (slice(None), slice(out_map.oh, out_map.oh + (P - 1) * out_map.stride + 1, out_map.stride),
                   slice(out_map.ow, out_map.ow + (Q - 1) * out_map.stride + 1, out_map.stride))
             if residual is not None:
                 out = out + residual[sl].to(_DT[0])
+        elif residual is not None:
+            out = out + residual.to(_DT[0])
+        if bn_bwd is not None:
+            bx, bsc, bsh, bmu, bis = bn_bwd
+            xb = (bx[sl] if sl is not None else bx).to(_DT[0])
+            out = out.to(y.dtype).to(_DT[0]) * ((xb * bsc + bsh) > 0).to(_DT[0])
+            gg, xh = out.reshape(-1, K), ((xb - bmu) * bis).reshape(-1, K)
+            stats.view(-1)[:K].add_(gg.sum(0))
+            stats.view(-1)[K:2 * K].add_((gg * xh).sum(0))
+        if sl is not None:
             y[sl] = out.to(y.dtype)
             return
-        if residual is not None:
-            out = out + residual.to(_DT[0])
         y.copy_(out)
-        if stats is not None:
+        if stats is not None and bn_bwd is None:
             yy = y.to(_DT[0]).reshape(-1, K)
             stats.view(-1)[:K].add_(yy.sum(0))
             stats.view(-1)[K:2 * K].add_((yy * yy).sum(0))

@@ -21,6 +21,8 @@ start bucket all-reduces while earlier layers are still back-propagating.
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 from typing import Callable, List, Optional
 
@@ -98,6 +100,8 @@ class Executor:
                  weight_decay: float = 2e-4, momentum: float = 0.9, params: ParamStore | None = None,
                  materialize_bn: Optional[bool] = None):
         self.spec, self.N, self.be = spec, batch, backend
+        # fuse each BN's backward reduction into the epilogue of the data-gradient conv feeding it
+        self.fuse_bn_bwd = os.environ.get("DRN_FUSE_BN_BWD", "1") == "1"
         self.device = torch.device(device)
         self.wd, self.mom = weight_decay, momentum
         self.is_hip = backend.name == "hip"
@@ -106,7 +110,6 @@ class Executor:
         # per BN by a streaming kernel (one extra read+write of the tensor, no per-element VALU
         # work in the MFMA loops). Measured on MI355X the materialised form is faster.
         if materialize_bn is None:
-            import os
             materialize_bn = os.environ.get("DRN_FUSE_BN_PROLOGUE", "0") != "1"
         self.materialize_bn = materialize_bn
         self.fdt = backend.acc_dtype
@@ -366,15 +369,20 @@ class Executor:
     def _view(self, buf, like):
         return buf[:like.numel()].view(like.shape)
 
-    def _bn_bwd(self, b: BNState, x, dy, dx, add=None, dpool=None, pool_hw=0):
-        """dx = BN-ReLU backward of (x -> relu(bn(x))) given dy = d/d relu-output; + add."""
+    def _bn_bwd(self, b: BNState, x, dy, dx, add=None, dpool=None, pool_hw=0, reduced=False):
+        """dx = BN-ReLU backward of (x -> relu(bn(x))) given dy = d/d relu-output; + add.
+        reduced: the producing data-gradient conv already ReLU-masked dy and accumulated the
+        per-channel sums into bn_part (fused epilogue), so only finalize + apply remain."""
         be = self.be
         M = x.numel() // b.bn.c
         part = self.bn_part
-        G = be.bn_bwd_reduce(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, part)
+        G = 1
+        if not reduced:
+            G = be.bn_bwd_reduce(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, part)
         coef = self.bn_coef[:3 * b.bn.c]
         be.bn_finalize_bwd(part, G, M, b.gamma, b.invstd, b.dgamma, b.dbeta, coef)
-        be.bn_bwd_apply(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, coef, add, dx)
+        be.bn_bwd_apply(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, coef, add, dx,
+                        relu=not reduced)
 
     def backward(self):
         be, sp = self.be, self.spec
@@ -408,11 +416,18 @@ class Executor:
         if self.grad_ready is not None:
             self.grad_ready(0)
 
-    def _dgrad(self, op: ConvOp, dy, dx, accumulate: bool):
+    def _dgrad(self, op: ConvOp, dy, dx, accumulate: bool, bn: Optional[BNState] = None, bn_x=None):
+        """Data gradient of `op` into dx (+= when accumulate). With bn set (requires a launch set
+        covering every dx element) the epilogue also performs that BN's backward reduction."""
         if not accumulate and not op.full_cover:
             self.be.zero_(dx)
+        fuse = None
+        if bn is not None:
+            assert op.full_cover
+            fuse = (bn_x, bn.scale, bn.shift, bn.mean, bn.invstd)
         for ph in op.dg:
-            self.be.conv_fwd(dy, ph.wt, dx, ph.geom, residual=dx if accumulate else None, out_map=ph.out_map)
+            self.be.conv_fwd(dy, ph.wt, dx, ph.geom, residual=dx if accumulate else None, out_map=ph.out_map,
+                             stats=self.bn_part if fuse is not None else None, bn_bwd=fuse)
 
     def _block_bwd(self, bp: BlockPlan, bufs, cur: int) -> int:
         """Back-propagates one block; bufs[cur] holds d(block output). Returns the index of the
@@ -429,16 +444,20 @@ class Executor:
             a_in, pro = self._cin(b)
             be.conv_wgrad(a_in, dy, op.dw, op.geom, in_bn=pro, ws=self.wgrad_ws)
             da = self._view(tgt, xin)        # d relu(bn(xin))
-            self._dgrad(op, dy, da, accumulate=False)
             add = None
-            if i == 0:
-                if bp.proj is not None:
-                    pj = bp.proj
-                    be.conv_wgrad(a_in, d_out, pj.dw, pj.geom, in_bn=pro, ws=self.wgrad_ws)
-                    self._dgrad(pj, d_out, da, accumulate=True)
-                else:
+            fuse = self.fuse_bn_bwd and op.full_cover
+            if i == 0 and bp.proj is not None:
+                # the projection's data gradient first, the main conv's accumulating one last so
+                # that its (full-cover, stride-1) epilogue can carry the fused BN reduction
+                pj = bp.proj
+                be.conv_wgrad(a_in, d_out, pj.dw, pj.geom, in_bn=pro, ws=self.wgrad_ws)
+                self._dgrad(pj, d_out, da, accumulate=False)
+                self._dgrad(op, dy, da, accumulate=True, bn=b if fuse else None, bn_x=xin)
+            else:
+                self._dgrad(op, dy, da, accumulate=False, bn=b if fuse else None, bn_x=xin)
+                if i == 0:
                     add = d_out              # identity shortcut
-            self._bn_bwd(b, xin, da, da, add=add)
+            self._bn_bwd(b, xin, da, da, add=add, reduced=fuse)
             dy, dy_buf = da, tgt
         return next(k for k, t in enumerate(bufs) if t is dy_buf)
 

@@ -94,7 +94,13 @@ def main():
                     ad = be.conv_args(dy, wt, dx, _dg(g, k, k))
                     ad.cfg = cfg
                     res_d.append((timeit(lambda: be.launch_conv(ad), a.iters), cfg))
+            res_w = []
+            for ns in (0, 2, 3):
+                be.forced_wgrad_ns = ns
+                res_w.append((timeit(lambda: be.conv_wgrad(x, dy, dw, g, in_bn=pro, ws=ws), a.iters), ns))
+            be.forced_wgrad_ns = None
             fmt = lambda r: " ".join(f"{c}:{t:.0f}" for t, c in r)
+            print(f"      wgrad best {min(res_w)} | {fmt(res_w)}", flush=True)
             print(f"sweep {kind} {cin}->{cout} k{k}s{s} @{H} x{cnt}: fwd best {min(res_f)} | {fmt(res_f)}", flush=True)
             if res_d:
                 print(f"      dgrad best {min(res_d)} | {fmt(res_d)}", flush=True)

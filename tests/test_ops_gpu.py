@@ -127,6 +127,35 @@ def test_conv_glds_out_map(hip, ref):
         assert rel(y, y_ref) < 1e-2, cfg
 
 
+@pytest.mark.parametrize("cfg", [100, 0, 3, 6])
+def test_conv_fused_bn_bwd_reduce(hip, ref, cfg):
+    """Data-gradient conv with the fused BN-backward epilogue (ReLU mask + sum g, sum g*xhat)."""
+    torch.manual_seed(11)
+    N, H, C, K = 2, 10, 64, 128
+    dy = bf(torch.randn(N, H, H, K))
+    wt = bf(torch.randn(C, 3, 3, K) * 0.05)
+    xb = bf(torch.randn(N, H, H, C))
+    sc, sh = torch.rand(C) + 0.5, torch.randn(C) * 0.3
+    mu, istd = torch.randn(C) * 0.1, torch.rand(C) + 0.5
+    res = bf(torch.randn(N, H, H, C))
+    g = ConvGeom(1, 1, 1)
+    y_ref = torch.zeros(N, H, H, C)
+    st_ref = torch.zeros(2 * C)
+    ref.conv_fwd(dy.float(), wt.float(), y_ref, g, residual=res.float(), stats=st_ref,
+                 bn_bwd=(xb.float(), sc, sh, mu, istd))
+    y = torch.zeros(N, H, H, C, dtype=torch.bfloat16, device="cuda")
+    st = torch.zeros(2, C, device="cuda")
+    a = hip.conv_args(dy.cuda(), wt.cuda(), y, g, residual=res.cuda(), stats=st,
+                      bn_bwd=(xb.cuda(), sc.cuda(), sh.cuda(), mu.cuda(), istd.cuda()))
+    a.cfg = cfg
+    hip.launch_conv(a)
+    torch.cuda.synchronize()
+    assert rel(y, y_ref) < 1e-2
+    s_hip = st.view(-1).cpu()
+    assert rel(s_hip[:C], st_ref[:C]) < 2e-2
+    assert rel(s_hip[C:], st_ref[C:]) < 2e-2
+
+
 @pytest.mark.parametrize("case", CONV_CASES[:-1])
 def test_conv_dgrad_matches_autograd(hip, case):
     N, H, W, C, K, R, s, p = case
@@ -167,6 +196,40 @@ def test_conv_wgrad(hip, ref, case, fused):
     ws = torch.zeros(max(1, hip.wgrad_ws_elems(N * P * P, K, R, R, C)), device="cuda")
     hip.conv_wgrad(x.cuda(), dy.cuda(), dw, g, in_bn=None if in_bn is None else (in_bn[0].cuda(), in_bn[1].cuda()),
                    ws=ws)
+    torch.cuda.synchronize()
+    assert rel(dw, dw_ref) < 1e-2
+
+
+WGRAD_GLDS_CASES = [
+    (2, 9, 9, 64, 64, 3, 1, 1),
+    (2, 8, 8, 128, 256, 1, 1, 0),
+    (3, 13, 13, 64, 128, 3, 2, 1),
+    (2, 16, 16, 8, 64, 7, 2, 3),      # stem: Ktot = 392 (partial k tile)
+    (2, 7, 7, 256, 72, 3, 1, 1),      # K % BCO != 0
+    (1, 6, 6, 32, 16, 3, 1, 1),       # narrow (64 x 64 tiles)
+]
+
+
+@pytest.mark.parametrize("case", WGRAD_GLDS_CASES)
+@pytest.mark.parametrize("ns", [0, 2, 3])
+def test_conv_wgrad_pipelines(hip, ref, case, ns):
+    """Register-staged (ns=0) and LDS-DMA (2/3 stages) weight-gradient kernels vs fp32."""
+    N, H, W, C, K, R, s, p = case
+    torch.manual_seed(7)
+    P = out_size(H, R, s, p)
+    x = bf(torch.randn(N, H, W, C))
+    dy = bf(torch.randn(N, P, P, K))
+    g = ConvGeom(stride=s, pad_h=p, pad_w=p)
+    dw_ref = torch.zeros(K, R, R, C)
+    ref.conv_wgrad(x.float(), dy.float(), dw_ref, g)
+    dw = torch.zeros(K, R, R, C, device="cuda")
+    ws = torch.zeros(max(1, hip.wgrad_ws_elems(N * P * P, K, R, R, C)), device="cuda")
+    old = hip.forced_wgrad_ns
+    hip.forced_wgrad_ns = ns
+    try:
+        hip.conv_wgrad(x.cuda(), dy.cuda(), dw, g, ws=ws)
+    finally:
+        hip.forced_wgrad_ns = old
     torch.cuda.synchronize()
     assert rel(dw, dw_ref) < 1e-2
 
