@@ -110,13 +110,114 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, int64_t nvec, int CV,
                                                        int relu) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if ((CV & (CV - 1)) == 0) {
+    // power-of-two C/8: the grid stride is a multiple of C/8, so this thread's 8 channels are
+    // fixed; keep scale/shift in registers
+    const int c = (int)(i0 & (CV - 1)) * 8;
+    float sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = scale[c + j];
+      sh[j] = shift[c + j];
+    }
+    for (int64_t i = i0; i < nvec; i += stride) {
+      float f[8];
+      unpack8(reinterpret_cast<const uint4*>(x)[i], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        f[j] = f[j] * sc[j] + sh[j];
+        if (relu) f[j] = fmaxf(f[j], 0.f);
+      }
+      reinterpret_cast<uint4*>(y)[i] = pack8(f);
+    }
+    return;
+  }
+  for (int64_t i = i0; i < nvec; i += stride) {
     const int c = (int)(i % CV) * 8;
     float f[8];
     unpack8(reinterpret_cast<const uint4*>(x)[i], f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       f[j] = f[j] * scale[c + j] + shift[c + j];
+      if (relu) f[j] = fmaxf(f[j], 0.f);
+    }
+    reinterpret_cast<uint4*>(y)[i] = pack8(f);
+  }
+}
+
+__device__ __forceinline__ void load8f(const float* p, float* f) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+__device__ __forceinline__ void store8f(float* p, const float* f) {
+  reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+  reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+}
+
+// Per-channel batch statistics -> (scale, shift, mean, invstd) in fp32 (the finalize math).
+__device__ __forceinline__ void bn_stats_to_affine(float s, float q, float count, float gamma, float beta, float eps,
+                                                   float& sc, float& sh, float& mean, float& invstd, float& var) {
+  mean = s / count;
+  var = fmaxf(q / count - mean * mean, 0.f);
+  invstd = 1.f / sqrtf(var + eps);
+  sc = gamma * invstd;
+  sh = beta - mean * sc;
+}
+
+// Finalize fused into the materialising apply: every thread derives scale/shift of its fixed
+// 8-channel group straight from the [2][C] sums (the grid stride is a multiple of C/8, a power
+// of two), block 0 publishes scale/shift/mean/invstd for the backward pass and updates the
+// moving averages. The sums are NOT zeroed here (other blocks still read them): the executor
+// clears the whole statistics arena once at the start of the step.
+__global__ __launch_bounds__(256) void bn_apply_stats_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                             const float* __restrict__ acc, float count,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, float eps,
+                                                             float momentum, float* __restrict__ run_mean,
+                                                             float* __restrict__ run_var, float* __restrict__ scale,
+                                                             float* __restrict__ shift, float* __restrict__ mean_out,
+                                                             float* __restrict__ invstd_out, int64_t nvec, int CV,
+                                                             int relu) {
+  const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int C = CV * 8;
+  const int c = (int)(i0 & (CV - 1)) * 8;  // CV is a power of two
+  // all per-channel inputs with 16-byte loads issued together (one latency, not eight)
+  float as[8], aq[8], ga[8], be[8], sc[8], sh[8];
+  load8f(acc + c, as);
+  load8f(acc + C + c, aq);
+  load8f(gamma + c, ga);
+  load8f(beta + c, be);
+  float mean[8], invstd[8], var[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    bn_stats_to_affine(as[j], aq[j], count, ga[j], be[j], eps, sc[j], sh[j], mean[j], invstd[j], var[j]);
+  if (blockIdx.x == 0 && threadIdx.x < CV) {
+    store8f(scale + c, sc);
+    store8f(shift + c, sh);
+    store8f(mean_out + c, mean);
+    store8f(invstd_out + c, invstd);
+    if (run_mean) {
+      float rm[8], rv[8];
+      load8f(run_mean + c, rm);
+      load8f(run_var + c, rv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float unbiased = count > 1.f ? var[j] * count / (count - 1.f) : var[j];
+        rm[j] = momentum * rm[j] + (1.f - momentum) * mean[j];
+        rv[j] = momentum * rv[j] + (1.f - momentum) * unbiased;
+      }
+      store8f(run_mean + c, rm);
+      store8f(run_var + c, rv);
+    }
+  }
+  for (int64_t i = i0; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
+    float f[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[i], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f[j] = f[j] * sc[j] + sh[j];
       if (relu) f[j] = fmaxf(f[j], 0.f);
     }
     reinterpret_cast<uint4*>(y)[i] = pack8(f);
@@ -243,6 +344,53 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(DySrc src, const bf16
   }
 }
 
+// bn_finalize_bwd fused into the apply: coefficients per thread from the [2][C] sums (sum g,
+// sum g*xhat), block 0 writes dbeta/dgamma. Same fixed-channel-group argument as above.
+__global__ __launch_bounds__(256) void bn_bwd_apply_stats_kernel(
+    DySrc src, const bf16_t* __restrict__ x, const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ acc, float count,
+    const float* __restrict__ gamma, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    const bf16_t* __restrict__ add, bf16_t* __restrict__ dx, int64_t nvec, int C, int relu) {
+  const int CV = C / 8;
+  const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int c = (int)(i0 & (CV - 1)) * 8;  // CV is a power of two
+  float sg[8], sgx[8], ga[8], k1[8], k2[8], k3[8], sc[8], sh[8], mu[8], is[8];
+  load8f(acc + c, sg);
+  load8f(acc + C + c, sgx);
+  load8f(gamma + c, ga);
+  load8f(invstd + c, is);
+  load8f(scale + c, sc);
+  load8f(shift + c, sh);
+  load8f(mean + c, mu);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    k1[j] = ga[j] * is[j];
+    k2[j] = sg[j] / count;
+    k3[j] = sgx[j] / count;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < CV) {
+    store8f(dbeta + c, sg);
+    store8f(dgamma + c, sgx);
+  }
+  for (int64_t i = i0; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = i / CV;
+    float fx[8], fd[8], fa[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[i], fx);
+    src.load(m, C, c, fd);
+    if (add) unpack8(reinterpret_cast<const uint4*>(add)[i], fa);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float yv = fx[j] * sc[j] + sh[j];
+      const float g = (relu && yv <= 0.f) ? 0.f : fd[j];
+      const float xh = (fx[j] - mu[j]) * is[j];
+      float v = k1[j] * (g - k2[j] - xh * k3[j]);
+      if (add) v += fa[j];
+      fd[j] = v;
+    }
+    reinterpret_cast<uint4*>(dx)[i] = pack8(fd);
+  }
+}
+
 static inline int grid_for(int64_t nvec) {
   int64_t b = (nvec + 255) / 256;
   if (b > 8192) b = 8192;
@@ -284,6 +432,33 @@ DRN_API int drn_bn_apply(const void* x, void* y, const float* scale, const float
   const int64_t nvec = M * (C / 8);
   hipLaunchKernelGGL(drn::bn_apply_kernel, dim3(drn::grid_for(nvec)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y,
                      scale, shift, nvec, C / 8, relu);
+  return (int)hipGetLastError();
+}
+
+static bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
+
+DRN_API int drn_bn_apply_stats(const void* x, void* y, const float* acc, float count, const float* gamma,
+                               const float* beta, float eps, float momentum, float* run_mean, float* run_var,
+                               float* scale, float* shift, float* mean, float* invstd, int64_t M, int C, int relu,
+                               hipStream_t s) {
+  if (C % 8 || !pow2(C / 8) || C / 8 > 256) return (int)hipErrorInvalidValue;
+  const int64_t nvec = M * (C / 8);
+  hipLaunchKernelGGL(drn::bn_apply_stats_kernel, dim3(drn::grid_for(nvec)), dim3(256), 0, s, (const bf16_t*)x,
+                     (bf16_t*)y, acc, count, gamma, beta, eps, momentum, run_mean, run_var, scale, shift, mean, invstd,
+                     nvec, C / 8, relu);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_bn_bwd_apply_stats(const void* dy, const float* dpool, int pool_hw, const void* x, const float* scale,
+                                   const float* shift, const float* mean, const float* invstd, const float* acc,
+                                   float count, const float* gamma, float* dgamma, float* dbeta, const void* add,
+                                   void* dx, int64_t M, int C, int relu, hipStream_t s) {
+  if (C % 8 || !pow2(C / 8) || C / 8 > 256) return (int)hipErrorInvalidValue;
+  const int64_t nvec = M * (C / 8);
+  drn::DySrc src{(const bf16_t*)dy, dpool, pool_hw};
+  hipLaunchKernelGGL(drn::bn_bwd_apply_stats_kernel, dim3(drn::grid_for(nvec)), dim3(256), 0, s, src,
+                     (const bf16_t*)x, scale, shift, mean, invstd, acc, count, gamma, dgamma, dbeta,
+                     (const bf16_t*)add, (bf16_t*)dx, nvec, C, relu);
   return (int)hipGetLastError();
 }
 

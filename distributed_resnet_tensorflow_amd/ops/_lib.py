@@ -73,6 +73,10 @@ _SIGS = {
     "drn_bn_finalize": ([c_p, c_int, c_int, c_f, c_p, c_p, c_f, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_int),
     "drn_bn_inference_params": ([c_int, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p], c_int),
     "drn_bn_apply": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_p], c_int),
+    "drn_bn_apply_stats": ([c_p, c_p, c_p, c_f, c_p, c_p, c_f, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_int,
+                            c_int, c_p], c_int),
+    "drn_bn_bwd_apply_stats": ([c_p, c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_i64,
+                                c_int, c_int, c_p], c_int),
     "drn_bn_bwd_reduce": ([c_p, c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p], c_int),
     "drn_bn_finalize_bwd": ([c_p, c_int, c_int, c_f, c_p, c_p, c_p, c_p, c_p, c_p], c_int),
     "drn_bn_bwd_apply": ([c_p, c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_p], c_int),

@@ -72,6 +72,13 @@ def tflip_table(descs):
     return torch.from_numpy(arr.view(np.uint8).copy()), len(descs), begin
 
 
+def _aligned16(*ts):
+    """The fused BN kernels read per-channel vectors with 16-byte loads."""
+    for t in ts:
+        if t is not None and t.data_ptr() % 16:
+            raise ValueError("per-channel BN buffers must be 16-byte aligned")
+
+
 @dataclass(frozen=True)
 class OutMap:
     """Strided output mapping of a phase of a stride-2 data gradient: the GEMM's P x Q grid lands
@@ -95,6 +102,19 @@ class _Common:
     @staticmethod
     def conv_stats_tiles(M, K):
         return 1
+
+    # Finalize fused into the apply kernels (HIP overrides with single kernels). Contract: the
+    # statistics accumulator is left unchanged (the executor clears its arena per step).
+    def bn_apply_stats(self, x, y, acc, count, gamma, beta, run_mean, run_var, scale, shift, mean, invstd,
+                       momentum, eps, relu=True):
+        self.bn_finalize(acc.clone(), 1, count, gamma, beta, run_mean, run_var, scale, shift, mean, invstd,
+                         momentum, eps, update_running=True)
+        self.bn_apply(x, y, scale, shift, relu=relu)
+
+    def bn_bwd_apply_stats(self, dy, dpool, pool_hw, x, scale, shift, mean, invstd, acc, count, gamma, dgamma,
+                           dbeta, add, dx, coef, relu=True):
+        self.bn_finalize_bwd(acc.clone(), 1, count, gamma, invstd, dgamma, dbeta, coef)
+        self.bn_bwd_apply(dy, dpool, pool_hw, x, scale, shift, mean, invstd, coef, add, dx, relu=relu)
 
 
 class HipBackend(_Common):
@@ -332,6 +352,26 @@ class HipBackend(_Common):
         C = x.shape[-1]
         _lib.check(self.L.drn_bn_apply(x.data_ptr(), y.data_ptr(), scale.data_ptr(), shift.data_ptr(),
                                        x.numel() // C, C, 1 if relu else 0, self.stream()), "drn_bn_apply")
+
+    def bn_apply_stats(self, x, y, acc, count, gamma, beta, run_mean, run_var, scale, shift, mean, invstd,
+                       momentum, eps, relu=True):
+        C = x.shape[-1]
+        _aligned16(acc, gamma, beta, run_mean, run_var, scale, shift, mean, invstd)
+        _lib.check(self.L.drn_bn_apply_stats(x.data_ptr(), y.data_ptr(), acc.data_ptr(), float(count),
+                                             gamma.data_ptr(), beta.data_ptr(), float(eps), float(momentum),
+                                             run_mean.data_ptr(), run_var.data_ptr(), scale.data_ptr(),
+                                             shift.data_ptr(), mean.data_ptr(), invstd.data_ptr(), x.numel() // C, C,
+                                             1 if relu else 0, self.stream()), "drn_bn_apply_stats")
+
+    def bn_bwd_apply_stats(self, dy, dpool, pool_hw, x, scale, shift, mean, invstd, acc, count, gamma, dgamma,
+                           dbeta, add, dx, coef=None, relu=True):
+        C = x.shape[-1]
+        _aligned16(acc, gamma, dgamma, dbeta, scale, shift, mean, invstd)
+        _lib.check(self.L.drn_bn_bwd_apply_stats(_ptr(dy), _ptr(dpool), pool_hw, x.data_ptr(), scale.data_ptr(),
+                                                 shift.data_ptr(), mean.data_ptr(), invstd.data_ptr(),
+                                                 acc.data_ptr(), float(count), gamma.data_ptr(), dgamma.data_ptr(),
+                                                 dbeta.data_ptr(), _ptr(add), dx.data_ptr(), x.numel() // C, C,
+                                                 1 if relu else 0, self.stream()), "drn_bn_bwd_apply_stats")
 
     def bn_bwd_reduce(self, dy, dpool, pool_hw, x, scale, shift, mean, invstd, part, relu=True):
         C = x.shape[-1]

@@ -54,6 +54,7 @@ class BNState:
     rows: int = 0                          # N*H*W of the normalised tensor
     src: Optional[torch.Tensor] = None     # the raw (pre-BN) tensor
     act: Optional[torch.Tensor] = None     # materialised relu(bn(src)) (materialize_bn mode)
+    bacc: Optional[torch.Tensor] = None    # backward sums [2][C] (sum g, sum g*xhat)
 
     @property
     def ss(self):
@@ -102,6 +103,11 @@ class Executor:
         self.spec, self.N, self.be = spec, batch, backend
         # fuse each BN's backward reduction into the epilogue of the data-gradient conv feeding it
         self.fuse_bn_bwd = os.environ.get("DRN_FUSE_BN_BWD", "1") == "1"
+        # BN finalize (forward and backward) folded into the streaming apply kernels
+        # (measured: a win in the backward apply, a loss in the forward apply, whose per-thread
+        # finalize prologue costs more than the separate C-thread finalize launch)
+        self.fuse_finalize = os.environ.get("DRN_FUSE_BN_FINALIZE", "1") == "1"
+        self.fuse_finalize_fwd = os.environ.get("DRN_FUSE_BN_FINALIZE_FWD", "0") == "1"
         self.device = torch.device(device)
         self.wd, self.mom = weight_decay, momentum
         self.is_hip = backend.name == "hip"
@@ -171,11 +177,22 @@ class Executor:
         return op, wt_off
 
     def _stats_for(self, M: int, C: int) -> tuple[torch.Tensor, int]:
-        return self._f32(2, C), 1
+        """A [2][C] statistics accumulator carved from the per-step-cleared arena."""
+        n = (2 * C + 15) // 16 * 16
+        if self._arena_off + n > self.stats_arena.numel():
+            raise RuntimeError("statistics arena exhausted")
+        t = self.stats_arena[self._arena_off:self._arena_off + 2 * C].view(2, C)
+        self._arena_off += n
+        return t, 1
 
     def _alloc(self):
         sp, N = self.spec, self.N
         be = self.be
+        # one arena for every BN statistics accumulator (forward sums and backward sums), cleared
+        # by a single fill at the start of each training step
+        all_c = [b.c for blk in sp.blocks for b in [blk.bn1] + list(blk.bns)] + [sp.final_bn.c, sp.stem.cout]
+        self.stats_arena = self._f32(sum(2 * ((2 * c + 15) // 16 * 16) for c in all_c) + 64)
+        self._arena_off = 0
         wt_descs, wt_off = [], 0
         self.stem_op, wt_off = self._conv_op(sp.stem, wt_descs, wt_off)
         img = sp.image_size
@@ -189,7 +206,7 @@ class Executor:
             ph = sp.pool_hw
             self.pool_out = self._act(N, ph, ph, sp.stem.cout)
             self.pool_arg = torch.zeros(N, ph, ph, sp.stem.cout, dtype=torch.uint8, device=self.device)
-            self.pool_stats, self.pool_G = self._f32(2, sp.stem.cout), 1
+            self.pool_stats, self.pool_G = self._stats_for(0, sp.stem.cout)
             x, x_stats, x_G = self.pool_out, self.pool_stats, self.pool_G
             self.stem_stats, self.stem_G = None, 0
         else:
@@ -252,6 +269,8 @@ class Executor:
             for bp in self.blocks:
                 for b in bp.bn:
                     b.act = self._act(*b.src.shape)
+        for b in [b for bp in self.blocks for b in bp.bn] + [self.final_bn]:
+            b.bacc = self._stats_for(0, b.bn.c)[0]
         self.last_out = x
         C, ncls = sp.final_c, sp.num_classes
         self.pooled = self._f32(N, C)
@@ -309,6 +328,10 @@ class Executor:
     # forward
     # ------------------------------------------------------------------------------------------
     def _bn_fwd(self, b: BNState, train: bool):
+        if train and b.act is not None and self.fuse_finalize_fwd:
+            self.be.bn_apply_stats(b.src, b.act, b.stats, b.rows, b.gamma, b.beta, b.run_mean, b.run_var, b.scale,
+                                   b.shift, b.mean, b.invstd, BN_DECAY, BN_EPSILON, relu=True)
+            return
         if train:
             self.be.bn_finalize(b.stats, b.G, b.rows, b.gamma, b.beta, b.run_mean, b.run_var, b.scale, b.shift,
                                 b.mean, b.invstd, BN_DECAY, BN_EPSILON, update_running=True)
@@ -326,6 +349,8 @@ class Executor:
     def forward(self, train: bool = True):
         """Runs the network on self.images/self.labels; fills loss_vec/correct (and dlogits)."""
         be, sp = self.be, self.spec
+        if train:
+            be.zero_(self.stats_arena)
         st = self.stem_op
         be.conv_fwd(self.images, st.w, self.stem_out, st.geom, stats=self.stem_stats if train else None)
         if sp.maxpool:
@@ -375,11 +400,15 @@ class Executor:
         per-channel sums into bn_part (fused epilogue), so only finalize + apply remain."""
         be = self.be
         M = x.numel() // b.bn.c
-        part = self.bn_part
+        part = b.bacc
         G = 1
         if not reduced:
             G = be.bn_bwd_reduce(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, part)
         coef = self.bn_coef[:3 * b.bn.c]
+        if self.fuse_finalize:
+            be.bn_bwd_apply_stats(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, part, M, b.gamma,
+                                  b.dgamma, b.dbeta, add, dx, coef=coef, relu=not reduced)
+            return
         be.bn_finalize_bwd(part, G, M, b.gamma, b.invstd, b.dgamma, b.dbeta, coef)
         be.bn_bwd_apply(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, coef, add, dx,
                         relu=not reduced)
@@ -427,7 +456,7 @@ class Executor:
             fuse = (bn_x, bn.scale, bn.shift, bn.mean, bn.invstd)
         for ph in op.dg:
             self.be.conv_fwd(dy, ph.wt, dx, ph.geom, residual=dx if accumulate else None, out_map=ph.out_map,
-                             stats=self.bn_part if fuse is not None else None, bn_bwd=fuse)
+                             stats=bn.bacc if fuse is not None else None, bn_bwd=fuse)
 
     def _block_bwd(self, bp: BlockPlan, bufs, cur: int) -> int:
         """Back-propagates one block; bufs[cur] holds d(block output). Returns the index of the
