@@ -36,6 +36,9 @@ struct DrnConvFwdArgs {
   // Kernel configuration for drn_conv_fwd2: -1 automatic, 0..7 an LDS-DMA tile configuration
   // (DRN_GLDS_CONFIGS), 100 the register-staged kernel.
   int32_t cfg;
+  // stats holds stats_rep replicas [rep][2][K]; block b adds into replica b % rep, so no
+  // address collects more than blocks/rep atomics (same-address float atomics serialize).
+  int32_t stats_rep;
   // Optional fused BatchNorm-backward reduction (data-gradient launches): when bn_x is set the
   // conv output v is d/d relu(bn(bn_x)); the epilogue stores the ReLU-masked gradient
   // g = v * [bn_x*scale+shift > 0] and accumulates stats[0][k] += g,

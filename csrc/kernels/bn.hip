@@ -4,9 +4,10 @@
 // `batch_norm_relu` (reference resnet_model_official.py:41-50: momentum 0.997, eps 1e-5,
 // center+scale, per-replica statistics, moving averages via UPDATE_OPS, resnet_model.py:119).
 //
-// Statistics flow: every reduction ends in a [2][C] fp32 accumulator (per-block register/LDS
-// reduction, then ONE atomic add per channel per block); the finalize kernels read it and zero
-// it again for the next step, so no memset is replayed and the finalize is C threads of O(1).
+// Statistics flow: every reduction ends in a [R][2][C] fp32 accumulator (per-block register/LDS
+// reduction, then ONE atomic add per channel per block into replica blockIdx % R, so no address
+// serializes more than blocks/R same-address atomics); the finalize kernels sum the replicas.
+// The executor clears all accumulators with one fill at the start of each step.
 //   forward  : sums -> drn_bn_finalize -> scale/shift (+ running stats update); the sums come
 //              from drn_bn_stats or straight from the producing convolution's epilogue
 //              (conv_fwd.hip `stats`); scale/shift are then applied inside the CONSUMER conv's
@@ -22,7 +23,7 @@ namespace drn {
 
 // x [M][C] -> acc[2][C] += (sum, sumsq)
 __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict__ x, float* __restrict__ part, int M,
-                                                       int C, int rows_per_block) {
+                                                       int C, int rows_per_block, int rep) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int CV = C / 8;
   const int tid = threadIdx.x;
@@ -59,22 +60,43 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict_
     const int cvv = c / 8, j = c % 8;
     float acc = 0.f;
     for (int r = 0; r < rpp; ++r) acc += red[(r * CV + cvv) * 16 + which * 8 + j];
-    atomicAdd(part + (size_t)which * C + c, acc);
+    atomicAdd(part + ((size_t)(blockIdx.x % rep) * 2 + which) * C + c, acc);
   }
 }
 
-// acc[2][C] -> scale/shift (+mean, invstd), running stats update. One thread per channel.
-__global__ void bn_finalize_kernel(float* __restrict__ part, int G, int C, float count,
+// acc[G][2][C] (G atomic-spreading replicas) -> scale/shift (+mean, invstd), running stats
+// update. Block = 64 channels x 4 replica groups (loads of all replicas in flight at once),
+// partial sums combined through LDS in a fixed order. The accumulator is not cleared here:
+// the executor clears the whole statistics arena once per step.
+__device__ __forceinline__ void sum_replicas(const float* __restrict__ part, int G, int C, float* s_out, float* q_out,
+                                             float (*red)[2][64]) {
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s = 0.f, q = 0.f;
+  if (c < C) {
+    for (int r = grp; r < G; r += 4) {
+      s += part[(size_t)r * 2 * C + c];
+      q += part[(size_t)r * 2 * C + C + c];
+    }
+  }
+  red[grp][0][cl] = s;
+  red[grp][1][cl] = q;
+  __syncthreads();
+  *s_out = (red[0][0][cl] + red[1][0][cl]) + (red[2][0][cl] + red[3][0][cl]);
+  *q_out = (red[0][1][cl] + red[1][1][cl]) + (red[2][1][cl] + red[3][1][cl]);
+}
+
+__global__ __launch_bounds__(256) void bn_finalize_kernel(float* __restrict__ part, int G, int C, float count,
                                    const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
                                    float momentum, float* __restrict__ run_mean, float* __restrict__ run_var,
                                    float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ mean_out,
                                    float* __restrict__ invstd_out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float* acc = part;
-  const double s = acc[c], q = acc[C + c];
-  acc[c] = 0.f;
-  acc[C + c] = 0.f;
+  __shared__ float red[4][2][64];
+  float sf, qf;
+  sum_replicas(part, G, C, &sf, &qf, red);
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if (threadIdx.x >= 64 || c >= C) return;
+  const double s = sf, q = qf;
   const double mean = s / count;
   double var = q / count - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -247,7 +269,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(DySrc src, const bf1
                                                             const float* __restrict__ shift,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd, float* __restrict__ part,
-                                                            int M, int C, int rows_per_block, int relu) {
+                                                            int M, int C, int rows_per_block, int relu, int rep) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int CV = C / 8;
   const int tid = threadIdx.x;
@@ -291,28 +313,26 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(DySrc src, const bf1
     const int cvv = ch / 8, j = ch % 8;
     float acc = 0.f;
     for (int r = 0; r < rpp; ++r) acc += red[(r * CV + cvv) * 16 + which * 8 + j];
-    atomicAdd(part + (size_t)which * C + ch, acc);
+    atomicAdd(part + ((size_t)(blockIdx.x % rep) * 2 + which) * C + ch, acc);
   }
 }
 
-// acc[2][C] (sum g, sum g*xhat; re-zeroed) -> dbeta, dgamma (written to the gradient buffer, scaled by
-// grad_scale and ACCUMULATED if accumulate) + apply coefficients coef[3][C]:
+// acc[G][2][C] (sum g, sum g*xhat) -> dbeta, dgamma + apply coefficients coef[3][C]:
 //   dx = k1 * (g - k2 - xhat * k3),  k1 = gamma*invstd, k2 = sum g / M, k3 = sum g*xhat / M
-__global__ void bn_finalize_bwd_kernel(float* __restrict__ part, int G, int C, float count,
+__global__ __launch_bounds__(256) void bn_finalize_bwd_kernel(float* __restrict__ part, int G, int C, float count,
                                        const float* __restrict__ gamma, const float* __restrict__ invstd,
                                        float* __restrict__ dgamma, float* __restrict__ dbeta,
                                        float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float* acc = part;
-  const double s = acc[c], sx = acc[C + c];
-  acc[c] = 0.f;
-  acc[C + c] = 0.f;
-  dbeta[c] = (float)s;
-  dgamma[c] = (float)sx;
+  __shared__ float red[4][2][64];
+  float sf, sxf;
+  sum_replicas(part, G, C, &sf, &sxf, red);
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if (threadIdx.x >= 64 || c >= C) return;
+  dbeta[c] = sf;
+  dgamma[c] = sxf;
   coef[c] = gamma[c] * invstd[c];
-  coef[C + c] = (float)(s / count);
-  coef[2 * C + c] = (float)(sx / count);
+  coef[C + c] = sf / count;
+  coef[2 * C + c] = sxf / count;
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(DySrc src, const bf16_t* __restrict__ x,
@@ -323,20 +343,39 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(DySrc src, const bf16
                                                            const float* __restrict__ coef,
                                                            const bf16_t* __restrict__ add, bf16_t* __restrict__ dx,
                                                            int64_t nvec, int C, int relu) {
+  // C/8 is a power of two (host-checked): the grid stride is a multiple of C/8, so every
+  // thread's 8 channels are fixed and all per-channel operands live in registers. The affine
+  // form dx = A*g + B*x + D folds k1*(g - k2 - (x-mu)*is*k3).
   const int CV = C / 8;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int c = (int)(i0 & (CV - 1)) * 8;
+  float sc[8], sh[8], A[8], B[8], D[8];
+  {
+    float mu[8], is[8], k1[8], k2[8], k3[8];
+    load8f(scale + c, sc);
+    load8f(shift + c, sh);
+    load8f(mean + c, mu);
+    load8f(invstd + c, is);
+    load8f(coef + c, k1);
+    load8f(coef + C + c, k2);
+    load8f(coef + 2 * C + c, k3);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      A[j] = k1[j];
+      B[j] = -k1[j] * k3[j] * is[j];
+      D[j] = -k1[j] * k2[j] + k1[j] * k3[j] * is[j] * mu[j];
+    }
+  }
+  for (int64_t i = i0; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t m = i / CV;
-    const int c = (int)(i - m * CV) * 8;
     float fx[8], fd[8], fa[8];
     unpack8(reinterpret_cast<const uint4*>(x)[i], fx);
     src.load(m, C, c, fd);
     if (add) unpack8(reinterpret_cast<const uint4*>(add)[i], fa);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float y = fx[j] * scale[c + j] + shift[c + j];
-      const float g = (relu && y <= 0.f) ? 0.f : fd[j];
-      const float xh = (fx[j] - mean[c + j]) * invstd[c + j];
-      float v = coef[c + j] * (g - coef[C + c + j] - xh * coef[2 * C + c + j]);
+      const float g = (relu && fx[j] * sc[j] + sh[j] <= 0.f) ? 0.f : fd[j];
+      float v = A[j] * g + B[j] * fx[j] + D[j];
       if (add) v += fa[j];
       fd[j] = v;
     }
@@ -400,20 +439,22 @@ static inline int grid_for(int64_t nvec) {
 
 }  // namespace drn
 
+static bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
+
 DRN_API int drn_bn_stats_blocks(int M, int C, int rows_per_block) { return (M + rows_per_block - 1) / rows_per_block; }
 
-DRN_API int drn_bn_stats(const void* x, float* part, int M, int C, int rows_per_block, hipStream_t s) {
-  if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
+DRN_API int drn_bn_stats(const void* x, float* part, int M, int C, int rows_per_block, int rep, hipStream_t s) {
+  if (C % 8 || C / 8 > 256 || rep < 1) return (int)hipErrorInvalidValue;
   const int G = (M + rows_per_block - 1) / rows_per_block;
   hipLaunchKernelGGL(drn::bn_stats_kernel, dim3(G), dim3(256), 256 * 16 * 4, s, (const bf16_t*)x, part, M, C,
-                     rows_per_block);
+                     rows_per_block, rep);
   return (int)hipGetLastError();
 }
 
 DRN_API int drn_bn_finalize(float* part, int G, int C, float count, const float* gamma, const float* beta,
                             float eps, float momentum, float* run_mean, float* run_var, float* scale, float* shift,
                             float* mean, float* invstd, hipStream_t s) {
-  hipLaunchKernelGGL(drn::bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, G, C, count, gamma, beta,
+  hipLaunchKernelGGL(drn::bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, G, C, count, gamma, beta,
                      eps, momentum, run_mean, run_var, scale, shift, mean, invstd);
   return (int)hipGetLastError();
 }
@@ -434,8 +475,6 @@ DRN_API int drn_bn_apply(const void* x, void* y, const float* scale, const float
                      scale, shift, nvec, C / 8, relu);
   return (int)hipGetLastError();
 }
-
-static bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
 
 DRN_API int drn_bn_apply_stats(const void* x, void* y, const float* acc, float count, const float* gamma,
                                const float* beta, float eps, float momentum, float* run_mean, float* run_var,
@@ -464,18 +503,18 @@ DRN_API int drn_bn_bwd_apply_stats(const void* dy, const float* dpool, int pool_
 
 DRN_API int drn_bn_bwd_reduce(const void* dy, const float* dpool, int pool_hw, const void* x, const float* scale,
                               const float* shift, const float* mean, const float* invstd, float* part, int M, int C,
-                              int rows_per_block, int relu, hipStream_t s) {
-  if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
+                              int rows_per_block, int relu, int rep, hipStream_t s) {
+  if (C % 8 || C / 8 > 256 || rep < 1) return (int)hipErrorInvalidValue;
   const int G = (M + rows_per_block - 1) / rows_per_block;
   drn::DySrc src{(const bf16_t*)dy, dpool, pool_hw};
   hipLaunchKernelGGL(drn::bn_bwd_reduce_kernel, dim3(G), dim3(256), 256 * 16 * 4, s, src, (const bf16_t*)x, scale,
-                     shift, mean, invstd, part, M, C, rows_per_block, relu);
+                     shift, mean, invstd, part, M, C, rows_per_block, relu, rep);
   return (int)hipGetLastError();
 }
 
 DRN_API int drn_bn_finalize_bwd(float* part, int G, int C, float count, const float* gamma,
                                 const float* invstd, float* dgamma, float* dbeta, float* coef, hipStream_t s) {
-  hipLaunchKernelGGL(drn::bn_finalize_bwd_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, G, C, count, gamma,
+  hipLaunchKernelGGL(drn::bn_finalize_bwd_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, G, C, count, gamma,
                      invstd, dgamma, dbeta, coef);
   return (int)hipGetLastError();
 }
@@ -483,7 +522,7 @@ DRN_API int drn_bn_finalize_bwd(float* part, int G, int C, float count, const fl
 DRN_API int drn_bn_bwd_apply(const void* dy, const float* dpool, int pool_hw, const void* x, const float* scale,
                              const float* shift, const float* mean, const float* invstd, const float* coef,
                              const void* add, void* dx, int64_t M, int C, int relu, hipStream_t s) {
-  if (C % 8) return (int)hipErrorInvalidValue;
+  if (C % 8 || !pow2(C / 8) || C / 8 > 256) return (int)hipErrorInvalidValue;
   const int64_t nvec = M * (C / 8);
   drn::DySrc src{(const bf16_t*)dy, dpool, pool_hw};
   hipLaunchKernelGGL(drn::bn_bwd_apply_kernel, dim3(drn::grid_for(nvec)), dim3(256), 0, s, src, (const bf16_t*)x,

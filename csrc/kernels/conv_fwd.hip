@@ -171,7 +171,8 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
       const int chh = cl >> 3, j = cl & 7;
       float s = 0.f;
       for (int t2 = chh; t2 < 256; t2 += CHR) s += red[t2 * 16 + which * 8 + j];
-      if (c0 + cl < a.K) atomicAdd(a.stats + (size_t)which * a.K + c0 + cl, s);
+      const int rep = a.stats_rep > 1 ? a.stats_rep : 1;
+      if (c0 + cl < a.K) atomicAdd(a.stats + ((size_t)(blockIdx.x % rep) * 2 + which) * a.K + c0 + cl, s);
     }
   }
 }

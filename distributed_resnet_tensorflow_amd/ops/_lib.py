@@ -44,7 +44,7 @@ class DrnConvFwdArgs(ctypes.Structure):
         ("P", c_int), ("Q", c_int), ("stride", c_int), ("pad_h", c_int), ("pad_w", c_int), ("dil", c_int),
         ("relu_in", c_int), ("tiles_p", c_int),
         ("out_H", c_int), ("out_W", c_int), ("out_stride", c_int), ("out_oh", c_int), ("out_ow", c_int),
-        ("cfg", c_int),
+        ("cfg", c_int), ("stats_rep", c_int),
         ("bn_x", c_p), ("bn_scale", c_p), ("bn_shift", c_p), ("bn_mean", c_p), ("bn_invstd", c_p),
     ]
 
@@ -69,7 +69,7 @@ _SIGS = {
     "drn_conv_wgrad": ([ctypes.POINTER(DrnConvWgradArgs), c_p], c_int),
     "drn_conv_wgrad2": ([ctypes.POINTER(DrnConvWgradArgs), c_p, c_int, c_p], c_int),
     "drn_splitk_reduce": ([c_p, c_p, c_i64, c_int, c_f, c_int, c_p], c_int),
-    "drn_bn_stats": ([c_p, c_p, c_int, c_int, c_int, c_p], c_int),
+    "drn_bn_stats": ([c_p, c_p, c_int, c_int, c_int, c_int, c_p], c_int),
     "drn_bn_finalize": ([c_p, c_int, c_int, c_f, c_p, c_p, c_f, c_f, c_p, c_p, c_p, c_p, c_p, c_p, c_p], c_int),
     "drn_bn_inference_params": ([c_int, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p], c_int),
     "drn_bn_apply": ([c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_p], c_int),
@@ -77,7 +77,8 @@ _SIGS = {
                             c_int, c_p], c_int),
     "drn_bn_bwd_apply_stats": ([c_p, c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_f, c_p, c_p, c_p, c_p, c_p, c_i64,
                                 c_int, c_int, c_p], c_int),
-    "drn_bn_bwd_reduce": ([c_p, c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p], c_int),
+    "drn_bn_bwd_reduce": ([c_p, c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_p],
+                          c_int),
     "drn_bn_finalize_bwd": ([c_p, c_int, c_int, c_f, c_p, c_p, c_p, c_p, c_p, c_p], c_int),
     "drn_bn_bwd_apply": ([c_p, c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_p], c_int),
     "drn_bnrelu_pool": ([c_p, c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p], c_int),

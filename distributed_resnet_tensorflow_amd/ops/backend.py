@@ -121,6 +121,9 @@ class HipBackend(_Common):
     name = "hip"
     act_dtype = torch.bfloat16
     acc_dtype = torch.float32
+    # replicas of every BN statistics accumulator: producer block b adds into replica b % 32,
+    # the finalize kernels sum them (same-address fp32 atomics serialize at ~15 ns each)
+    stats_replicas = 32
 
     def __init__(self, device="cuda"):
         self.device = torch.device(device)
@@ -163,7 +166,9 @@ class HipBackend(_Common):
         if out_map is not None:
             a.out_H, a.out_W, a.out_stride, a.out_oh, a.out_ow = oH, oW, out_map.stride, out_map.oh, out_map.ow
         if stats is not None:
-            assert stats.numel() >= 2 * K and stats.dtype == torch.float32, "stats accumulator must be fp32 [2][K]"
+            assert stats.numel() % (2 * K) == 0 and stats.dtype == torch.float32, \
+                "stats accumulator must be fp32 [rep][2][K]"
+            a.stats_rep = stats.numel() // (2 * K)
         if bn_bwd is not None:
             assert stats is not None, "fused BN-backward reduction accumulates into stats"
             bx, bsc, bsh, bmu, bis = bn_bwd
@@ -197,7 +202,7 @@ class HipBackend(_Common):
         oh = a.out_H if a.out_stride else a.P
         ow = a.out_W if a.out_stride else a.Q
         y = torch.empty(N * oh * ow * K, dtype=torch.bfloat16, device=self.device)
-        st = torch.zeros(2 * K, dtype=torch.float32, device=self.device)
+        st = torch.zeros(max(1, a.stats_rep) * 2 * K, dtype=torch.float32, device=self.device)  # all replicas
         t = _lib.DrnConvFwdArgs()
         ctypes.memmove(ctypes.addressof(t), ctypes.addressof(a), ctypes.sizeof(a))
         t.y = y.data_ptr()
@@ -326,12 +331,13 @@ class HipBackend(_Common):
         return rpb
 
     def bn_stats(self, x, part):
-        """part[2][C] += (sum, sumsq) over rows of x."""
+        """part[R][2][C] += (sum, sumsq) over rows of x (block b into replica b % R); returns R."""
         C = x.shape[-1]
         M = x.numel() // C
         rpb = self.bn_rows_per_block(M, C)
-        _lib.check(self.L.drn_bn_stats(x.data_ptr(), part.data_ptr(), M, C, rpb, self.stream()), "drn_bn_stats")
-        return 1
+        _lib.check(self.L.drn_bn_stats(x.data_ptr(), part.data_ptr(), M, C, rpb, part.numel() // (2 * C),
+                                       self.stream()), "drn_bn_stats")
+        return part.numel() // (2 * C)
 
     def bn_finalize(self, part, G, count, gamma, beta, run_mean, run_var, scale, shift, mean, invstd,
                     momentum, eps, update_running=True):
@@ -379,8 +385,9 @@ class HipBackend(_Common):
         rpb = self.bn_rows_per_block(M, C)
         _lib.check(self.L.drn_bn_bwd_reduce(_ptr(dy), _ptr(dpool), pool_hw, x.data_ptr(), scale.data_ptr(),
                                             shift.data_ptr(), mean.data_ptr(), invstd.data_ptr(), part.data_ptr(),
-                                            M, C, rpb, 1 if relu else 0, self.stream()), "drn_bn_bwd_reduce")
-        return 1
+                                            M, C, rpb, 1 if relu else 0, part.numel() // (2 * C), self.stream()),
+                   "drn_bn_bwd_reduce")
+        return part.numel() // (2 * C)
 
     def bn_finalize_bwd(self, part, G, count, gamma, invstd, dgamma, dbeta, coef):
         _lib.check(self.L.drn_bn_finalize_bwd(part.data_ptr(), G, gamma.numel(), float(count), gamma.data_ptr(),
@@ -507,6 +514,7 @@ def _dilate(xc, dil):
 
 class RefBackend(_Common):
     name = "ref"
+    stats_replicas = 1
 
     def __init__(self, device="cpu", dtype=torch.float32):
         self.device = torch.device(device)

@@ -54,7 +54,8 @@ class BNState:
     rows: int = 0                          # N*H*W of the normalised tensor
     src: Optional[torch.Tensor] = None     # the raw (pre-BN) tensor
     act: Optional[torch.Tensor] = None     # materialised relu(bn(src)) (materialize_bn mode)
-    bacc: Optional[torch.Tensor] = None    # backward sums [2][C] (sum g, sum g*xhat)
+    bacc: Optional[torch.Tensor] = None    # backward sums [R][2][C] (sum g, sum g*xhat)
+    bG: int = 1                            # replicas of bacc
 
     @property
     def ss(self):
@@ -106,7 +107,7 @@ class Executor:
         # BN finalize (forward and backward) folded into the streaming apply kernels
         # (measured: a win in the backward apply, a loss in the forward apply, whose per-thread
         # finalize prologue costs more than the separate C-thread finalize launch)
-        self.fuse_finalize = os.environ.get("DRN_FUSE_BN_FINALIZE", "1") == "1"
+        self.fuse_finalize = os.environ.get("DRN_FUSE_BN_FINALIZE", "0") == "1"
         self.fuse_finalize_fwd = os.environ.get("DRN_FUSE_BN_FINALIZE_FWD", "0") == "1"
         self.device = torch.device(device)
         self.wd, self.mom = weight_decay, momentum
@@ -177,13 +178,15 @@ class Executor:
         return op, wt_off
 
     def _stats_for(self, M: int, C: int) -> tuple[torch.Tensor, int]:
-        """A [2][C] statistics accumulator carved from the per-step-cleared arena."""
-        n = (2 * C + 15) // 16 * 16
+        """A [R][2][C] statistics accumulator (R = the backend's atomic-spreading replicas)
+        carved from the per-step-cleared arena."""
+        R = self.stats_rep
+        n = (2 * C * R + 15) // 16 * 16
         if self._arena_off + n > self.stats_arena.numel():
             raise RuntimeError("statistics arena exhausted")
-        t = self.stats_arena[self._arena_off:self._arena_off + 2 * C].view(2, C)
+        t = self.stats_arena[self._arena_off:self._arena_off + 2 * C * R].view(R, 2, C)
         self._arena_off += n
-        return t, 1
+        return t, R
 
     def _alloc(self):
         sp, N = self.spec, self.N
@@ -191,7 +194,8 @@ class Executor:
         # one arena for every BN statistics accumulator (forward sums and backward sums), cleared
         # by a single fill at the start of each training step
         all_c = [b.c for blk in sp.blocks for b in [blk.bn1] + list(blk.bns)] + [sp.final_bn.c, sp.stem.cout]
-        self.stats_arena = self._f32(sum(2 * ((2 * c + 15) // 16 * 16) for c in all_c) + 64)
+        self.stats_rep = int(getattr(be, "stats_replicas", 1))
+        self.stats_arena = self._f32(sum(2 * ((2 * c * self.stats_rep + 15) // 16 * 16) for c in all_c) + 64)
         self._arena_off = 0
         wt_descs, wt_off = [], 0
         self.stem_op, wt_off = self._conv_op(sp.stem, wt_descs, wt_off)
@@ -270,7 +274,7 @@ class Executor:
                 for b in bp.bn:
                     b.act = self._act(*b.src.shape)
         for b in [b for bp in self.blocks for b in bp.bn] + [self.final_bn]:
-            b.bacc = self._stats_for(0, b.bn.c)[0]
+            b.bacc, b.bG = self._stats_for(0, b.bn.c)
         self.last_out = x
         C, ncls = sp.final_c, sp.num_classes
         self.pooled = self._f32(N, C)
@@ -328,7 +332,7 @@ class Executor:
     # forward
     # ------------------------------------------------------------------------------------------
     def _bn_fwd(self, b: BNState, train: bool):
-        if train and b.act is not None and self.fuse_finalize_fwd:
+        if train and b.act is not None and self.fuse_finalize_fwd and b.G == 1:
             self.be.bn_apply_stats(b.src, b.act, b.stats, b.rows, b.gamma, b.beta, b.run_mean, b.run_var, b.scale,
                                    b.shift, b.mean, b.invstd, BN_DECAY, BN_EPSILON, relu=True)
             return
@@ -401,11 +405,11 @@ class Executor:
         be = self.be
         M = x.numel() // b.bn.c
         part = b.bacc
-        G = 1
+        G = b.bG
         if not reduced:
             G = be.bn_bwd_reduce(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, part)
         coef = self.bn_coef[:3 * b.bn.c]
-        if self.fuse_finalize:
+        if self.fuse_finalize and G == 1:
             be.bn_bwd_apply_stats(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, part, M, b.gamma,
                                   b.dgamma, b.dbeta, add, dx, coef=coef, relu=not reduced)
             return

@@ -97,14 +97,14 @@ def test_conv_fwd_glds_configs(hip, ref, case, cfg):
     st_ref = torch.zeros(2 * K)
     ref.conv_fwd(x.float(), w.float(), y_ref, g, residual=res.float(), stats=st_ref)
     y = torch.zeros(N, P, P, K, dtype=torch.bfloat16, device="cuda")
-    st = torch.zeros(2, K, device="cuda")
+    st = torch.zeros(3, 2, K, device="cuda")  # 3 atomic-spreading replicas
     a = hip.conv_args(x.cuda(), w.cuda(), y, g, residual=res.cuda(), stats=st)
-    assert hip.L.drn_conv_glds_ok(a) == 1
+    assert hip.L.drn_conv_glds_ok(a) == 1 and a.stats_rep == 3
     a.cfg = cfg
     hip.launch_conv(a)
     torch.cuda.synchronize()
     assert rel(y, y_ref) < 1e-2
-    s_hip = st.view(-1).cpu()
+    s_hip = st.sum(0).view(-1).cpu()
     assert rel(s_hip[:K], st_ref[:K]) < 2e-2
     assert rel(s_hip[K:], st_ref[K:]) < 2e-2
 
