@@ -53,9 +53,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DRN_BENCH_BACKEND=gloo + DRN_BENCH_ONE_DEVICE=1 rehearse the multi-rank code path with every
+    # rank on cuda:0 (a one-GPU box); production runs use RCCL, one GPU per rank
+    backend = os.environ.get("DRN_BENCH_BACKEND", "nccl")
+    if os.environ.get("DRN_BENCH_ONE_DEVICE") == "1":
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from distributed_resnet_tensorflow_amd.models.spec import build_spec
     from distributed_resnet_tensorflow_amd.ops.backend import HipBackend
