@@ -31,13 +31,30 @@ def _free_port() -> int:
     return p
 
 
-def _spawn(nproc: int, cmd: List[str], port: int, base_env: dict) -> List[subprocess.Popen]:
+def _spawn(nproc: int, cmd: List[str], port: int, base_env: dict, nnodes: int = 1, node_rank: int = 0,
+           log_dir: str = "", tag: str = "", pid_file: str = "") -> List[subprocess.Popen]:
     procs = []
-    for r in range(nproc):
+    world = nproc * nnodes
+    host = socket.gethostname()
+    for lr in range(nproc):
+        r = node_rank * nproc + lr
         env = dict(base_env)
-        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_WORLD_SIZE=str(nproc),
-                   MASTER_ADDR=env.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=str(port))
-        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
+        env.update(RANK=str(r), LOCAL_RANK=str(lr), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(nproc),
+                   NODE_RANK=str(node_rank), MASTER_ADDR=env.get("MASTER_ADDR", "127.0.0.1"),
+                   MASTER_PORT=str(port))
+        out = None
+        if log_dir:
+            # per-process log, named like the reference launcher's worker.$JOB.$host-port.log
+            os.makedirs(log_dir, exist_ok=True)
+            out = open(os.path.join(log_dir, f"worker.{tag or 'job'}.{host}-{r}.log"), "ab")
+        procs.append(subprocess.Popen(cmd, env=env, start_new_session=True, stdout=out,
+                                      stderr=subprocess.STDOUT if out else None))
+        if out:
+            out.close()
+    if pid_file:
+        with open(pid_file, "a") as f:
+            for p in procs:
+                f.write(f"{p.pid}\n")
     return procs
 
 
@@ -60,12 +77,19 @@ def _kill_all(procs, grace: float = 10.0):
             p.wait()
 
 
-def run(nproc: int, cmd: List[str], max_restarts: int = 0, poll: float = 0.5) -> int:
+def run(nproc: int, cmd: List[str], max_restarts: int = 0, poll: float = 0.5, nnodes: int = 1, node_rank: int = 0,
+        log_dir: str = "", tag: str = "", pid_file: str = "") -> int:
+    """Run nproc ranks of `cmd` on this node (ranks node_rank*nproc ... of nnodes*nproc).
+    Multi-node jobs need a fixed MASTER_ADDR/MASTER_PORT (the first node); a failed rank ends
+    this node's ranks and the launcher exits non-zero (resubmission resumes from the
+    checkpoint); single-node jobs restart in place up to max_restarts times."""
     base_env = dict(os.environ)
     attempt = 0
+    if nnodes > 1 and not base_env.get("MASTER_PORT"):
+        raise SystemExit("multi-node launch needs MASTER_ADDR and MASTER_PORT")
     while True:
         port = int(base_env.get("MASTER_PORT", "0")) or _free_port()
-        procs = _spawn(nproc, cmd, port, base_env)
+        procs = _spawn(nproc, cmd, port, base_env, nnodes, node_rank, log_dir, tag, pid_file)
         failed = None
         try:
             while True:
@@ -83,7 +107,7 @@ def run(nproc: int, cmd: List[str], max_restarts: int = 0, poll: float = 0.5) ->
         rank, code = failed
         print(f"[drn.launch] rank {rank} exited with code {code}; tearing down the job", file=sys.stderr, flush=True)
         _kill_all(procs)
-        if attempt >= max_restarts:
+        if attempt >= max_restarts or nnodes > 1:
             return code if code > 0 else 1
         attempt += 1
         print(f"[drn.launch] restart {attempt}/{max_restarts} (resuming from the latest checkpoint)",
@@ -95,11 +119,23 @@ def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--nproc", "--nproc_per_node", type=int, default=1)
     ap.add_argument("--max_restarts", type=int, default=0)
+    ap.add_argument("--nnodes", type=int, default=1)
+    ap.add_argument("--node_rank", type=int, default=0)
+    ap.add_argument("--master_addr", default=None)
+    ap.add_argument("--master_port", type=int, default=0)
+    ap.add_argument("--log_dir", default="", help="write worker.<tag>.<host>-<rank>.log files here")
+    ap.add_argument("--tag", default="", help="job tag used in log file names (e.g. $SLURM_JOB_ID)")
+    ap.add_argument("--pid_file", default="", help="append child PIDs here (scripts/kill.sh reads it)")
     ap.add_argument("script")
     ap.add_argument("args", nargs=argparse.REMAINDER)
     a = ap.parse_args(argv)
+    if a.master_addr:
+        os.environ["MASTER_ADDR"] = a.master_addr
+    if a.master_port:
+        os.environ["MASTER_PORT"] = str(a.master_port)
     cmd = [sys.executable, a.script] + a.args
-    return run(a.nproc, cmd, a.max_restarts)
+    return run(a.nproc, cmd, a.max_restarts, nnodes=a.nnodes, node_rank=a.node_rank, log_dir=a.log_dir,
+               tag=a.tag, pid_file=a.pid_file)
 
 
 if __name__ == "__main__":
