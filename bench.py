@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--dataset", default="imagenet", choices=["imagenet", "cifar10"])
     ap.add_argument("--resnet_size", type=int, default=50)
+    ap.add_argument("--width", type=int, default=1, help="bottleneck width multiplier (2 = Wide-ResNet-50-2)")
     ap.add_argument("--batch_size", type=int, default=128, help="per-GPU batch")
     ap.add_argument("--graph", type=int, default=-1, help="capture the step in a HIP graph (-1: auto)")
     ap.add_argument("--bucket_mb", type=float, default=25.0)
@@ -71,7 +72,7 @@ def main():
     from distributed_resnet_tensorflow_amd.runtime.graph import StepGraph
     from distributed_resnet_tensorflow_amd.parallel.engine import DataParallelEngine
 
-    spec = build_spec(args.dataset, args.resnet_size)
+    spec = build_spec(args.dataset, args.resnet_size, width=args.width)
     be = HipBackend("cuda")
     wd = 2e-4 if args.dataset == "cifar10" else 1e-4
     ex = Executor(spec, args.batch_size, be, "cuda", seed=1234, weight_decay=wd)
@@ -122,11 +123,14 @@ def main():
     img_s = args.batch_size * world * args.steps / dt
     loss = float(ex.loss_vec.float().mean())
     if rank == 0:
-        base = BASELINE_IMG_S.get(args.dataset, {}).get(world)
+        base = BASELINE_IMG_S.get(args.dataset, {}).get(world) if (args.width == 1 and args.resnet_size == 50) else None
         model = f"resnet{args.resnet_size}_v2_{args.dataset}" if args.dataset == "imagenet" else \
             f"cifar10_resnet{args.resnet_size}_v2"
+        if args.width > 1:
+            model = f"wide_resnet{args.resnet_size}_{args.width}_{args.dataset}"
         out = {
-            "metric": "images/sec (whole node) ResNet-50 bs=128/GPU",
+            "metric": "images/sec (whole node) ResNet-50 bs=128/GPU" if (args.width == 1 and args.batch_size == 128)
+            else f"images/sec (whole node) {model} bs={args.batch_size}/GPU",
             "value": round(img_s, 2),
             "unit": "images/sec",
             "n_gpus": world,
