@@ -104,6 +104,16 @@ class Executor:
         self.spec, self.N, self.be = spec, batch, backend
         # fuse each BN's backward reduction into the epilogue of the data-gradient conv feeding it
         self.fuse_bn_bwd = os.environ.get("DRN_FUSE_BN_BWD", "1") == "1"
+        # debug mode: synchronous finiteness checks after every block (forward and backward)
+        self.check_nan = os.environ.get("DRN_CHECK_NAN", "0") == "1"
+        # deterministic mode (DRN_DETERMINISTIC=1): bitwise-reproducible steps -- one statistics
+        # slot per producer workgroup (no two atomics ever meet) and the unfused BN-backward
+        # reduction (the stride-2 data-gradient phases would share slots)
+        self.deterministic = os.environ.get("DRN_DETERMINISTIC", "0") == "1"
+        if self.deterministic:
+            self.fuse_bn_bwd = False
+            if hasattr(backend, "autotune"):
+                backend.autotune = False  # timing-dependent tile choices change per-tile partial sums
         # BN finalize (forward and backward) folded into the streaming apply kernels
         # (measured: a win in the backward apply, a loss in the forward apply, whose per-thread
         # finalize prologue costs more than the separate C-thread finalize launch)
@@ -177,10 +187,33 @@ class Executor:
         op = ConvOp(c, g, P.compute_w(name), phases, P.g(name), s.offset, full)
         return op, wt_off
 
+    def _bn_shapes(self):
+        """(rows, channels) of every statistics accumulator the plan allocates (upper bound)."""
+        sp, N = self.spec, self.N
+        hs = sp.stem_hw
+        out = [(N * hs * hs, sp.stem.cout)]
+        if sp.maxpool:
+            out.append((N * sp.pool_hw * sp.pool_hw, sp.stem.cout))
+        for blk in sp.blocks:
+            hw = blk.in_hw
+            out.append((N * hw * hw, blk.in_c))              # bn1 backward sums
+            for b, c in zip(blk.bns, blk.convs[:-1]):
+                hw = c.out_hw(hw)
+                out += [(N * hw * hw, c.cout)] * 2           # forward + backward sums
+            out.append((N * blk.out_hw * blk.out_hw, blk.out_c))
+        out.append((N * sp.blocks[-1].out_hw ** 2, sp.final_c))
+        return out
+
+    def _det_replicas(self, M: int, C: int) -> int:
+        """Deterministic mode: one replica per producer workgroup (the most workgroups any conv
+        tile config or BN reduction launches for an M x C tensor), so every accumulator slot
+        receives exactly one atomic add and the finalize sums the slots in a fixed order."""
+        return max(((M + 63) // 64) * ((C + 63) // 64), 1024)
+
     def _stats_for(self, M: int, C: int) -> tuple[torch.Tensor, int]:
         """A [R][2][C] statistics accumulator (R = the backend's atomic-spreading replicas)
         carved from the per-step-cleared arena."""
-        R = self.stats_rep
+        R = self._det_replicas(M, C) if self.deterministic else self.stats_rep
         n = (2 * C * R + 15) // 16 * 16
         if self._arena_off + n > self.stats_arena.numel():
             raise RuntimeError("statistics arena exhausted")
@@ -195,7 +228,11 @@ class Executor:
         # by a single fill at the start of each training step
         all_c = [b.c for blk in sp.blocks for b in [blk.bn1] + list(blk.bns)] + [sp.final_bn.c, sp.stem.cout]
         self.stats_rep = int(getattr(be, "stats_replicas", 1))
-        self.stats_arena = self._f32(sum(2 * ((2 * c * self.stats_rep + 15) // 16 * 16) for c in all_c) + 64)
+        if self.deterministic:
+            arena = 64 + sum(2 * ((2 * c * self._det_replicas(m, c) + 15) // 16 * 16) for m, c in self._bn_shapes())
+        else:
+            arena = sum(2 * ((2 * c * self.stats_rep + 15) // 16 * 16) for c in all_c) + 64
+        self.stats_arena = self._f32(arena)
         self._arena_off = 0
         wt_descs, wt_off = [], 0
         self.stem_op, wt_off = self._conv_op(sp.stem, wt_descs, wt_off)
@@ -210,7 +247,7 @@ class Executor:
             ph = sp.pool_hw
             self.pool_out = self._act(N, ph, ph, sp.stem.cout)
             self.pool_arg = torch.zeros(N, ph, ph, sp.stem.cout, dtype=torch.uint8, device=self.device)
-            self.pool_stats, self.pool_G = self._stats_for(0, sp.stem.cout)
+            self.pool_stats, self.pool_G = self._stats_for(N * sp.pool_hw * sp.pool_hw, sp.stem.cout)
             x, x_stats, x_G = self.pool_out, self.pool_stats, self.pool_G
             self.stem_stats, self.stem_G = None, 0
         else:
@@ -274,7 +311,7 @@ class Executor:
                 for b in bp.bn:
                     b.act = self._act(*b.src.shape)
         for b in [b for bp in self.blocks for b in bp.bn] + [self.final_bn]:
-            b.bacc, b.bG = self._stats_for(0, b.bn.c)
+            b.bacc, b.bG = self._stats_for(b.rows, b.bn.c)
         self.last_out = x
         C, ncls = sp.final_c, sp.num_classes
         self.pooled = self._f32(N, C)
@@ -365,6 +402,8 @@ class Executor:
                 be.bn_stats(self.pool_out, self.pool_stats)
         for bp in self.blocks:
             self._block_fwd(bp, train)
+            if self.check_nan:
+                self._check(bp.out, f"forward output of block {bp.blk.stage}.{bp.blk.index}")
         fb = self.final_bn
         self._bn_fwd(fb, train)
         be.pool_bnrelu(self.last_out, fb.scale, fb.shift, self.pooled, relu=True)
@@ -372,6 +411,20 @@ class Executor:
         be.sgemm(0, 1, N, ncls, C, 1.0, self.pooled, C, self.dense_w, C, 0.0, self.logits, ncls, bias=self.dense_b)
         be.softmax_xent(self.logits, self.labels, 1.0 / N, self.dlogits if train else None, self.loss_vec,
                         self.correct)
+        if self.check_nan:
+            self._check(self.loss_vec, "cross-entropy")
+
+    def _check(self, t: torch.Tensor, what: str):
+        """DRN_CHECK_NAN=1 debug mode: synchronous finiteness check naming the failing stage."""
+        if not bool(torch.isfinite(t.float()).all()):
+            raise FloatingPointError(f"non-finite values in {what}")
+
+    def check_gradients(self):
+        """Names every trainable variable whose gradient is not finite (debug mode)."""
+        bad = [s.name for s in self.P.slots
+               if not bool(torch.isfinite(self.P.grad[s.offset:s.offset + s.numel]).all())]
+        if bad:
+            raise FloatingPointError(f"non-finite gradients: {bad[:8]}{' ...' if len(bad) > 8 else ''}")
 
     def _block_fwd(self, bp: BlockPlan, train: bool):
         be = self.be
@@ -434,6 +487,8 @@ class Executor:
         cur = 0  # index of the buffer holding d_out
         for bp in reversed(self.blocks):
             cur = self._block_bwd(bp, bufs, cur)
+            if self.check_nan:
+                self._check(self._view(bufs[cur], bp.x), f"input gradient of block {bp.blk.stage}.{bp.blk.index}")
             if self.grad_ready is not None:
                 self.grad_ready(bp.grad_lo)
         d_x0 = self._view(bufs[cur], self.blocks[0].x)
@@ -514,6 +569,8 @@ class Executor:
             self.set_lr(lr)
         self.forward(train=True)
         self.backward()
+        if self.check_nan:
+            self.check_gradients()
         if allreduce is not None:
             allreduce()
         self.apply_gradients(grad_scale)

@@ -98,7 +98,7 @@ class TrainingSession:
         """One synchronous training step on the batch already in ex.images / ex.labels."""
         self.cur_lr = self.lr.lr_for_step()
         self.ex.set_lr(self.cur_lr)
-        if self.use_graph:
+        if self.use_graph and not self.ex.check_nan:  # the debug checks synchronize: no capture
             if self._graph is None:
                 self._graph = StepGraph(self._step_body, warmup=1)  # warm-up = this real step
             else:

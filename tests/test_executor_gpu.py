@@ -141,3 +141,24 @@ def test_graph_replay_matches_eager():
     # BN statistics use fp32 atomics (order-nondeterministic in the last bits), so replay and
     # eager agree to rounding, not bitwise
     assert rel(outs[1], outs[0]) < 1e-2
+
+
+def test_deterministic_mode_is_bitwise_reproducible(monkeypatch):
+    """DRN_DETERMINISTIC=1: two executors, same seed and batch, two training steps each ->
+    bitwise-identical weights, momentum and BN moving statistics (catches races as
+    nondeterminism)."""
+    monkeypatch.setenv("DRN_DETERMINISTIC", "1")
+    spec, N = cifar_resnet_v2(14), 16
+    outs = []
+    for _ in range(2):
+        ex = Executor(spec, N, HipBackend(), "cuda", seed=3)
+        g = torch.Generator().manual_seed(9)
+        ex.images.zero_()
+        ex.images[..., :3] = torch.randn(N, 32, 32, 3, generator=g).bfloat16().cuda()
+        ex.labels.copy_(torch.randint(0, 10, (N,), generator=g, dtype=torch.int32))
+        for _ in range(2):
+            ex.train_step(lr=0.1)
+        torch.cuda.synchronize()
+        outs.append((ex.P.master.clone(), ex.P.momentum.clone(), ex.P.bn_state.clone()))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
