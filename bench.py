@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--batch_size", type=int, default=128, help="per-GPU batch")
     ap.add_argument("--graph", type=int, default=-1, help="capture the step in a HIP graph (-1: auto)")
     ap.add_argument("--bucket_mb", type=float, default=25.0)
+    ap.add_argument("--allreduce", default="rccl", choices=["rccl", "p2p", "auto"])
     args = ap.parse_args()
 
     import torch
@@ -76,7 +77,7 @@ def main():
     be = HipBackend("cuda")
     wd = 2e-4 if args.dataset == "cifar10" else 1e-4
     ex = Executor(spec, args.batch_size, be, "cuda", seed=1234, weight_decay=wd)
-    eng = DataParallelEngine(ex, bucket_mb=args.bucket_mb) if world > 1 else None
+    eng = DataParallelEngine(ex, bucket_mb=args.bucket_mb, allreduce=args.allreduce) if world > 1 else None
     if eng is not None:
         eng.broadcast_parameters()
     # synthetic data of the benchmark shape: fixed device batch (no host input pipeline)

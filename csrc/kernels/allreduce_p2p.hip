@@ -1,0 +1,129 @@
+// allreduce_p2p.hip — one-shot peer-to-peer gradient all-reduce over xGMI (single node).
+//
+// The reference averaged gradients through TF parameter servers or Horovod's NCCL all-reduce
+// (resnet_model.py:108-116). RCCL rings are per-link bound and pay a multi-step
+// latency that dominates small buckets (CIFAR ResNet's 3 MB of fp32 gradients). Here every GPU
+// maps its peers' gradient buffers (HIP IPC, opened by the host runtime) and reduces a bucket in
+// ONE kernel: out[i] = sum over ranks r of in_r[i], reading all 7 peers' slices concurrently
+// over the 7 point-to-point xGMI links (one-shot: each GPU reads (W-1)/W more bytes than a
+// ring but in one hop).
+//
+// Synchronisation (no host round trips, HIP-graph capturable; the epoch lives in device memory):
+//   ready: after a bucket's gradient is complete on the stream, drn_p2p_signal writes the epoch
+//          into slot [bucket][READY][my rank] of every peer's flag array (system-scope release,
+//          preceded by an L2 write-back so peers read the gradient from memory);
+//   reduce: every block polls its LOCAL flag array until all ranks' READY >= epoch, performs a
+//          system-scope acquire (cache invalidate), then reduces with 16-byte loads;
+//   done:   after all buckets, drn_p2p_signal(DONE); before the next step writes the gradient
+//          buffer, drn_p2p_wait(DONE) — no rank overwrites an input a peer may still be reading.
+// Every poll is bounded (DRN_P2P_SPIN_LIMIT iterations): on timeout the kernel records an error
+// code and exits, so a missing peer can never hang the GPU; the host checks the error word.
+#include "drn_common.h"
+
+#ifndef DRN_P2P_SPIN_LIMIT
+#define DRN_P2P_SPIN_LIMIT (1 << 26)
+#endif
+
+namespace drn {
+
+constexpr int P2P_MAX_RANKS = 8;
+constexpr int P2P_READY = 0, P2P_DONE = 1;
+
+struct P2PArgs {
+  float* out;                           // local output (never aliases an input)
+  const float* in[P2P_MAX_RANKS];       // every rank's gradient bucket (index = rank), mapped
+  unsigned* flags_local;                // this rank's flag array [slots][2][8]
+  unsigned* flags_peer[P2P_MAX_RANKS];  // every rank's flag array (remote mappings)
+  const unsigned* epoch;                // device-resident step epoch (>= 1)
+  int* err;                             // error word (0 = ok)
+  int64_t n;                            // elements in the bucket (multiple of 4)
+  int world, rank, slot, pad_;
+};
+
+__device__ __forceinline__ unsigned flag_load(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ bool wait_all(const P2PArgs& a, int kind, unsigned e) {
+  const unsigned* f = a.flags_local + (size_t)(a.slot * 2 + kind) * P2P_MAX_RANKS;
+  for (int it = 0; it < DRN_P2P_SPIN_LIMIT; ++it) {
+    bool ok = true;
+    for (int r = 0; r < a.world; ++r) ok = ok && flag_load(f + r) >= e;
+    if (ok) return true;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return false;
+}
+
+// kind = READY or DONE: publish this rank's epoch for `slot` to every rank (incl. itself).
+__global__ void p2p_signal_kernel(P2PArgs a, int kind) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const unsigned e = *a.epoch;
+  // make every earlier write of this device (the gradient kernels) visible system-wide
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  for (int r = 0; r < a.world; ++r) {
+    unsigned* f = a.flags_peer[r] + (size_t)(a.slot * 2 + kind) * P2P_MAX_RANKS + a.rank;
+    __hip_atomic_store(f, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__global__ __launch_bounds__(256) void p2p_reduce_kernel(P2PArgs a) {
+  __shared__ int ok;
+  if (threadIdx.x == 0) {
+    ok = wait_all(a, P2P_READY, *a.epoch) ? 1 : 0;
+    if (!ok) atomicExch(a.err, 1);
+  }
+  __syncthreads();
+  if (!ok) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // peers' gradient bytes, not stale cached lines
+  const int64_t n4 = a.n / 4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 s = reinterpret_cast<const float4*>(a.in[0])[i];
+    for (int r = 1; r < a.world; ++r) {
+      const float4 v = reinterpret_cast<const float4*>(a.in[r])[i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    reinterpret_cast<float4*>(a.out)[i] = s;
+  }
+}
+
+// Wait until every rank published DONE for `slot` at the previous epoch, then advance the
+// device epoch (one thread; launched once per step before the gradient buffer is rewritten).
+__global__ void p2p_wait_kernel(P2PArgs a, unsigned* epoch_rw) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const unsigned e = *epoch_rw;
+  if (e > 0 && !wait_all(a, P2P_DONE, e)) atomicExch(a.err, 2);
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
+  *epoch_rw = e + 1;
+}
+
+}  // namespace drn
+
+static bool p2p_check(const drn::P2PArgs* a) {
+  if (a->world < 1 || a->world > drn::P2P_MAX_RANKS || a->rank < 0 || a->rank >= a->world) return false;
+  if (a->n % 4) return false;
+  for (int r = 0; r < a->world; ++r)
+    if (a->in[r] == nullptr || a->flags_peer[r] == nullptr) return false;
+  return a->out != nullptr && a->flags_local != nullptr && a->epoch != nullptr && a->err != nullptr;
+}
+
+DRN_API int drn_p2p_signal(const drn::P2PArgs* a, int kind, hipStream_t s) {
+  if (!p2p_check(a)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(drn::p2p_signal_kernel, dim3(1), dim3(64), 0, s, *a, kind);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_p2p_reduce(const drn::P2PArgs* a, int blocks, hipStream_t s) {
+  if (!p2p_check(a)) return (int)hipErrorInvalidValue;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(drn::p2p_reduce_kernel, dim3(blocks), dim3(256), 0, s, *a);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_p2p_wait(const drn::P2PArgs* a, unsigned* epoch_rw, hipStream_t s) {
+  if (!p2p_check(a)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(drn::p2p_wait_kernel, dim3(1), dim3(64), 0, s, *a, epoch_rw);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_p2p_args_size() { return (int)sizeof(drn::P2PArgs); }

@@ -30,19 +30,19 @@ namespace drn {
 // epi_prefetch() computes those output offsets and issues the 16-byte loads of the residual
 // and of the fused-BN-backward input BEFORE the main loop, so their latency hides behind the
 // MFMA work instead of stalling the epilogue (short-K launches are otherwise dominated by it).
-template <int BP, int BC>
+template <int BP, int BC, int NT = 256>
 struct EpiPre {
   static constexpr int CHR = BC / 8;  // output 16-byte chunks per pixel row
-  static constexpr int RPI = 256 / CHR;
+  static constexpr int RPI = NT / CHR;
   static constexpr int IT = BP / RPI;
   int off[IT];     // element offset of the chunk, -1 when outside the output
   uint4 res[IT];
   uint4 bx[IT];
 };
 
-template <int BP, int BC>
-__device__ __forceinline__ void epi_prefetch(const DrnConvFwdArgs& a, int m0, int c0, int M, EpiPre<BP, BC>& e) {
-  using E = EpiPre<BP, BC>;
+template <int BP, int BC, int NT = 256>
+__device__ __forceinline__ void epi_prefetch(const DrnConvFwdArgs& a, int m0, int c0, int M, EpiPre<BP, BC, NT>& e) {
+  using E = EpiPre<BP, BC, NT>;
   const int tid = threadIdx.x;
   const int ch = tid % E::CHR;
   const int c = c0 + ch * 8;
@@ -76,10 +76,10 @@ __device__ __forceinline__ void epi_prefetch(const DrnConvFwdArgs& a, int m0, in
 // written as whole 2*BC-byte pixel rows per wave instruction (fully coalesced). Optional
 // residual add, optional strided output map, optional per-channel sum/sumsq for the next BN,
 // or (bn_x set) the fused BN-backward reduction with ReLU-masked output.
-template <int BP, int BC, int WP, int WC, int MI, int MJ>
+template <int BP, int BC, int WP, int WC, int MI, int MJ, int NT = 256>
 __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* smem, f32x4_t (&acc)[MI][MJ], int wp,
-                                              int wc, int m0, int c0, int M, const EpiPre<BP, BC>& e) {
-  using E = EpiPre<BP, BC>;
+                                              int wc, int m0, int c0, int M, const EpiPre<BP, BC, NT>& e) {
+  using E = EpiPre<BP, BC, NT>;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   constexpr int CF = BC / 4;   // fp32 16-byte chunks per staged row
@@ -159,7 +159,7 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
   }
   if (want_stats) {
     __syncthreads();
-    float* red = tile;  // [256][16]
+    float* red = tile;  // [NT][16]
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       red[tid * 16 + j] = ssum[j];
@@ -170,7 +170,7 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
       const int cl = tid >> 1, which = tid & 1;
       const int chh = cl >> 3, j = cl & 7;
       float s = 0.f;
-      for (int t2 = chh; t2 < 256; t2 += CHR) s += red[t2 * 16 + which * 8 + j];
+      for (int t2 = chh; t2 < NT; t2 += CHR) s += red[t2 * 16 + which * 8 + j];
       const int rep = a.stats_rep > 1 ? a.stats_rep : 1;
       if (c0 + cl < a.K) atomicAdd(a.stats + ((size_t)(blockIdx.x % rep) * 2 + which) * a.K + c0 + cl, s);
     }
@@ -411,17 +411,19 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BP, int BC, int WAVES_P, int NS>
-__global__ __launch_bounds__(256) void conv_fwd_glds_kernel(DrnConvFwdArgs a, const void* __restrict__ zero) {
-  constexpr int WAVES_C = 4 / WAVES_P;
+template <int BP, int BC, int WAVES_P, int NS, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a, const void* __restrict__ zero) {
+  constexpr int NT = NW * 64;
+  constexpr int WAVES_C = NW / WAVES_P;
   constexpr int WP = BP / WAVES_P, WC = BC / WAVES_C;
   constexpr int MI = WC / 16, MJ = WP / 16;
   constexpr int ROWB = 128;                 // 64 bf16 of k per LDS row
   constexpr int STAGE = (BC + BP) * ROWB;
-  constexpr int GA = BC / 32, GB = BP / 32;  // glds wave-instructions per stage (8 rows each)
+  constexpr int GA = BC / (8 * NW), GB = BP / (8 * NW);  // glds wave-instructions per stage (8 rows each)
   constexpr int G = GA + GB;
   constexpr int D = NS - 1;                 // stages in flight ahead of the computing one
-  static_assert(WAVES_P * WAVES_C == 4 && MI >= 1 && MJ >= 1, "4 waves");
+  static_assert(WAVES_P * WAVES_C == NW && MI >= 1 && MJ >= 1, "wave layout");
+  static_assert(GA * 8 * NW == BC && GB * 8 * NW == BP, "rows must split evenly over the waves");
   static_assert(NS >= 2 && G * (D > 1 ? D - 1 : 1) < 64, "pipeline depth");
 
   extern __shared__ __attribute__((aligned(1024))) char smem[];
@@ -445,7 +447,7 @@ __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(DrnConvFwdArgs a, co
   const bf16_t* wsrc[GA];
 #pragma unroll
   for (int i = 0; i < GA; ++i) {
-    const int row = 32 * i + 8 * wave + lrow;
+    const int row = 8 * NW * i + 8 * wave + lrow;
     const int lc = (lane & 7) ^ ((row >> 1) & 7);
     const int c = c0 + row;
     wsrc[i] = c < a.K ? reinterpret_cast<const bf16_t*>(a.w) + (size_t)c * Ktot + lc * 8 : nullptr;
@@ -453,7 +455,7 @@ __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(DrnConvFwdArgs a, co
   int boff[GB], bh[GB], bw[GB];
 #pragma unroll
   for (int i = 0; i < GB; ++i) {
-    const int row = 32 * i + 8 * wave + lrow;
+    const int row = 8 * NW * i + 8 * wave + lrow;
     const int lc = (lane & 7) ^ ((row >> 1) & 7);  // (BC + row) has the same bits 1..3
     const int m = m0 + row;
     if (m < M) {
@@ -479,7 +481,7 @@ __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(DrnConvFwdArgs a, co
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
       const void* src = wsrc[i] ? (const void*)(wsrc[i] + ik) : zero;
-      glds16(src, st + (32 * i + 8 * wave) * ROWB);
+      glds16(src, st + (8 * NW * i + 8 * wave) * ROWB);
     }
     const int tap_off = (ir * a.W + is) * C + ici;
 #pragma unroll
@@ -487,7 +489,7 @@ __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(DrnConvFwdArgs a, co
       const int h = bh[i] + ir, w = bw[i] + is;
       const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
       const void* src = ok ? (const void*)(xg + (boff[i] + tap_off)) : zero;
-      glds16(src, st + (BC + 32 * i + 8 * wave) * ROWB);
+      glds16(src, st + (BC + 8 * NW * i + 8 * wave) * ROWB);
     }
     ik += 64;
     ici += 64;
@@ -518,8 +520,8 @@ __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(DrnConvFwdArgs a, co
   const int swz = (fr >> 1) & 7;  // rows of a fragment group are 16-aligned: bits 1..3 = fr's
 
   const int T = Ktot / 64;
-  EpiPre<BP, BC> epre;
-  epi_prefetch<BP, BC>(a, m0, c0, M, epre);  // residual / BN inputs in flight during the main loop
+  EpiPre<BP, BC, NT> epre;
+  epi_prefetch<BP, BC, NT>(a, m0, c0, M, epre);  // residual / BN inputs in flight during the main loop
 #pragma unroll
   for (int s = 0; s < D; ++s)
     if (s < T) issue(s);
@@ -549,15 +551,16 @@ __global__ __launch_bounds__(256) void conv_fwd_glds_kernel(DrnConvFwdArgs a, co
     asm volatile("" ::: "memory");
   }
   __syncthreads();  // all fragment reads done before the epilogue reuses the LDS
-  static_assert(BP * BC * 4 <= NS * STAGE, "epilogue tile must fit the staging LDS");
-  conv_epilogue<BP, BC, WP, WC, MI, MJ>(a, smem, acc, wp, wc, m0, c0, M, epre);
+  // (the launcher sizes the dynamic LDS for max(NS * STAGE, BP * BC * 4))
+  conv_epilogue<BP, BC, WP, WC, MI, MJ, NT>(a, smem, acc, wp, wc, m0, c0, M, epre);
 }
 
-template <int BP, int BC, int WAVES_P, int NS>
+template <int BP, int BC, int WAVES_P, int NS, int NW = 4>
 static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
-  constexpr int LDS = NS * (BC + BP) * 128;
+  constexpr int LDS0 = NS * (BC + BP) * 128;
+  constexpr int LDS = LDS0 > BP * BC * 4 ? LDS0 : BP * BC * 4;  // epilogue staging tile
   static bool attr_set = false;
-  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS>;
+  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS, NW>;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
@@ -566,27 +569,31 @@ static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t str
   const int tiles_p = (M + BP - 1) / BP;
   const int tiles_c = (a->K + BC - 1) / BC;
   a->tiles_p = tiles_p;
-  hipLaunchKernelGGL(kern, dim3(tiles_p * tiles_c), dim3(256), LDS, stream, *a, zero);
+  hipLaunchKernelGGL(kern, dim3(tiles_p * tiles_c), dim3(NW * 64), LDS, stream, *a, zero);
   return (int)hipGetLastError();
 }
 
 // Tile configurations of the LDS-DMA kernel (index = DRN conv config id, also used by the
 // host-side autotuner): {BP, BC, WAVES_P, NS}.
 #define DRN_GLDS_CONFIGS(X)  \
-  X(0, 128, 128, 2, 2)       \
-  X(1, 128, 128, 2, 3)       \
-  X(2, 128, 128, 2, 4)       \
-  X(3, 256, 64, 4, 2)        \
-  X(4, 256, 64, 4, 3)        \
-  X(5, 128, 64, 2, 3)        \
-  X(6, 64, 128, 1, 3)        \
-  X(7, 64, 64, 2, 4)
+  X(0, 128, 128, 2, 2, 4)    \
+  X(1, 128, 128, 2, 3, 4)    \
+  X(2, 128, 128, 2, 4, 4)    \
+  X(3, 256, 64, 4, 2, 4)     \
+  X(4, 256, 64, 4, 3, 4)     \
+  X(5, 128, 64, 2, 3, 4)     \
+  X(6, 64, 128, 1, 3, 4)     \
+  X(7, 64, 64, 2, 4, 4)      \
+  X(8, 256, 128, 4, 2, 8)    \
+  X(9, 256, 128, 4, 3, 8)    \
+  X(10, 128, 256, 2, 2, 8)   \
+  X(11, 128, 256, 2, 3, 8)
 
 static int launch_glds_cfg(int cfg, DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
   switch (cfg) {
-#define DRN_X(id, bp, bc, wpv, ns) \
-  case id:                         \
-    return launch_conv_glds<bp, bc, wpv, ns>(a, zero, s);
+#define DRN_X(id, bp, bc, wpv, ns, nw) \
+  case id:                             \
+    return launch_conv_glds<bp, bc, wpv, ns, nw>(a, zero, s);
     DRN_GLDS_CONFIGS(DRN_X)
 #undef DRN_X
     default:
@@ -596,8 +603,8 @@ static int launch_glds_cfg(int cfg, DrnConvFwdArgs* a, const void* zero, hipStre
 
 static int glds_cfg_bp(int cfg) {
   switch (cfg) {
-#define DRN_X(id, bp, bc, wpv, ns) \
-  case id:                         \
+#define DRN_X(id, bp, bc, wpv, ns, nw) \
+  case id:                             \
     return bp;
     DRN_GLDS_CONFIGS(DRN_X)
 #undef DRN_X
@@ -667,7 +674,7 @@ DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
 }
 
 DRN_API int drn_conv_glds_cfg_bp(int cfg) { return drn::glds_cfg_bp(cfg); }
-DRN_API int drn_conv_glds_num_cfgs() { return 8; }
+DRN_API int drn_conv_glds_num_cfgs() { return 12; }
 DRN_API int drn_conv_glds_default_cfg(const DrnConvFwdArgs* a) { return drn::glds_default_cfg(a); }
 
 DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s) {

@@ -221,7 +221,8 @@ def define_reference_flags(flag_values: FlagValues = FLAGS, **defaults) -> FlagV
     I("log_every_n_steps", 20, "Logging period in steps (CIFAR 20, ImageNet 40).", fv)
     I("max_to_keep", 5, "Checkpoints kept in log_root (TF Saver default 5).", fv)
     S("profile_steps", "", "a:b -> roctx-mark and torch-profile steps a..b.", fv)
-    S("allreduce", "rccl", "Gradient all-reduce backend: rccl (GPU) / gloo (CPU).", fv)
+    S("allreduce", "rccl", "Gradient all-reduce: rccl (RCCL ring/tree over xGMI; gloo on CPU), p2p (one-shot "
+      "HIP-IPC peer kernel, one node), auto (p2p when the gradient is <= 64 MB).", fv)
     Fl("bucket_mb", 25.0, "Gradient all-reduce bucket size (MB of fp32).", fv)
     I("fault_inject_step", -1, "Kill this process at the given global step (fault-injection tests).", fv)
     I("fault_inject_rank", 0, "Rank that --fault_inject_step applies to.", fv)

@@ -33,7 +33,8 @@ import torch.distributed as dist
 
 
 class DataParallelEngine:
-    def __init__(self, executor, bucket_mb: float = 25.0, mode: str = "sync", group=None):
+    def __init__(self, executor, bucket_mb: float = 25.0, mode: str = "sync", group=None,
+                 allreduce: str = "rccl", p2p_max_mb: float = 64.0):
         self.ex = executor
         self.P = executor.P
         self.group = group
@@ -41,6 +42,17 @@ class DataParallelEngine:
         self.rank = dist.get_rank(group)
         self.mode = mode
         self.buckets = self._make_buckets(int(bucket_mb * (1 << 20) // 4))
+        # --allreduce: rccl | p2p (one-shot HIP IPC kernel, parallel/p2p.py) | auto (p2p when the
+        # whole gradient is small -- latency-bound CIFAR buckets -- and the job is one GPU node)
+        self.p2p = None
+        total_mb = self.P.total * 4 / (1 << 20)
+        want = allreduce == "p2p" or (allreduce == "auto" and total_mb <= p2p_max_mb)
+        if want and self.P.grad.is_cuda and mode == "sync" and self.world <= 8 \
+                and dist.get_backend(group) in ("nccl", "gloo"):
+            from .p2p import P2PAllReduce
+            if len(self.buckets) + 1 >= 64:
+                self.buckets = self._make_buckets(int(self.P.total // 60) + 1)
+            self.p2p = P2PAllReduce(self.P.grad, group)
         self.works: List = []
         self.launched = [False] * len(self.buckets)
         self.frontier = self.P.total
@@ -69,6 +81,8 @@ class DataParallelEngine:
         self.works = []
         self.launched = [False] * len(self.buckets)
         self.frontier = self.P.total
+        if self.p2p is not None:
+            self.p2p.begin_step()
         if self.mode == "sync":
             self.ex.grad_ready = self._on_ready
         else:
@@ -76,6 +90,10 @@ class DataParallelEngine:
 
     def _launch(self, i: int, buf: Optional[torch.Tensor] = None):
         lo, hi = self.buckets[i]
+        if self.p2p is not None:
+            self.p2p.reduce_bucket(i, lo, hi)
+            self.launched[i] = True
+            return
         t = (self.P.grad if buf is None else buf)[lo:hi]
         self.works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
         self.launched[i] = True
@@ -96,6 +114,9 @@ class DataParallelEngine:
                 w.wait()
             self.works = []
             self.ex.grad_ready = None
+            if self.p2p is not None:
+                self.p2p.end_step()
+                return self.p2p.out
             return self.P.grad
         # delayed (async-PS analog): finish last step's exchange, start this step's
         for w in self.works:

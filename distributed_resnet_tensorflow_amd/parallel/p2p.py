@@ -1,0 +1,173 @@
+"""One-shot peer-to-peer gradient all-reduce over xGMI (HIP IPC + csrc/kernels/allreduce_p2p.hip).
+
+SURVEY §5.8 / §7.2 step 7: for small buckets (CIFAR ResNet's ~3 MB of fp32 gradients) a ring
+all-reduce pays W-1 latency-bound steps per bucket; here each GPU maps every peer's gradient
+buffer once (hipIpcGetMemHandle / hipIpcOpenMemHandle, handles exchanged over the existing
+process group) and reduces a bucket in a single kernel that reads all peers concurrently. The
+synchronisation is device-side (epoch flags in IPC-mapped memory), so the whole step, comm
+included, stays capturable in one HIP graph. Large buckets are better served by RCCL; the
+engine chooses per bucket with --allreduce=auto.
+
+Limits: one node, <= 8 ranks, fp32 buckets whose element count is a multiple of 4.
+"""
+from __future__ import annotations
+
+import ctypes
+import pickle
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _lib
+
+MAX_RANKS = 8
+N_SLOTS = 64          # ready slots (one per bucket) + the DONE slot 0
+_HIP = None
+
+
+class _IpcHandle(ctypes.Structure):
+    _fields_ = [("reserved", ctypes.c_char * 64)]
+
+
+class P2PArgs(ctypes.Structure):
+    _fields_ = [
+        ("out", ctypes.c_void_p),
+        ("inp", ctypes.c_void_p * MAX_RANKS),
+        ("flags_local", ctypes.c_void_p),
+        ("flags_peer", ctypes.c_void_p * MAX_RANKS),
+        ("epoch", ctypes.c_void_p),
+        ("err", ctypes.c_void_p),
+        ("n", ctypes.c_int64),
+        ("world", ctypes.c_int), ("rank", ctypes.c_int), ("slot", ctypes.c_int), ("pad_", ctypes.c_int),
+    ]
+
+
+def _hip():
+    global _HIP
+    if _HIP is None:
+        h = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
+        h.hipIpcGetMemHandle.argtypes = [ctypes.POINTER(_IpcHandle), ctypes.c_void_p]
+        h.hipIpcOpenMemHandle.argtypes = [ctypes.POINTER(ctypes.c_void_p), _IpcHandle, ctypes.c_uint]
+        h.hipIpcCloseMemHandle.argtypes = [ctypes.c_void_p]
+        h.hipMemGetAddressRange.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+                                            ctypes.c_void_p]
+        for f in ("hipIpcGetMemHandle", "hipIpcOpenMemHandle", "hipIpcCloseMemHandle", "hipMemGetAddressRange"):
+            getattr(h, f).restype = ctypes.c_int
+        _HIP = h
+    return _HIP
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with hipError {rc}")
+
+
+def _export(t: torch.Tensor):
+    """(ipc handle bytes, byte offset of t inside its allocation)."""
+    h = _hip()
+    base, size = ctypes.c_void_p(), ctypes.c_size_t()
+    _check(h.hipMemGetAddressRange(ctypes.byref(base), ctypes.byref(size), ctypes.c_void_p(t.data_ptr())),
+           "hipMemGetAddressRange")
+    handle = _IpcHandle()
+    _check(h.hipIpcGetMemHandle(ctypes.byref(handle), base), "hipIpcGetMemHandle")
+    return bytes(handle.reserved), t.data_ptr() - base.value
+
+
+class P2PAllReduce:
+    """Maps every rank's `grad` (and flag words) and reduces buckets of it into `out`."""
+
+    def __init__(self, grad: torch.Tensor, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if self.world > MAX_RANKS:
+            raise ValueError("the P2P all-reduce supports one node of <= 8 ranks")
+        self.L = _lib.lib()
+        if self.L.drn_p2p_args_size() != ctypes.sizeof(P2PArgs):
+            raise RuntimeError("P2PArgs layout mismatch between Python and the kernel library")
+        self.grad = grad
+        self.comm = torch.cuda.Stream(device=grad.device)
+        dev = grad.device
+        self.out = torch.zeros_like(grad)
+        self.flags = torch.zeros(N_SLOTS * 2 * MAX_RANKS, dtype=torch.int32, device=dev)
+        self.epoch = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        mine = (_export(grad), _export(self.flags))
+        allh = [None] * self.world
+        dist.all_gather_object(allh, pickle.dumps(mine), group=group)
+        self._opened = []
+        self.in_ptr, self.flag_ptr = [], []
+        h = _hip()
+        for r, blob in enumerate(allh):
+            (gh, goff), (fh, foff) = pickle.loads(blob)
+            if r == self.rank:
+                self.in_ptr.append(grad.data_ptr())
+                self.flag_ptr.append(self.flags.data_ptr())
+                continue
+            ptrs = []
+            for hb, off in ((gh, goff), (fh, foff)):
+                hd = _IpcHandle()
+                hd.reserved = hb
+                p = ctypes.c_void_p()
+                _check(h.hipIpcOpenMemHandle(ctypes.byref(p), hd, 1), "hipIpcOpenMemHandle")  # lazy peer access
+                self._opened.append(p.value)
+                ptrs.append(p.value + off)
+            self.in_ptr.append(ptrs[0])
+            self.flag_ptr.append(ptrs[1])
+        dist.barrier(group=group)
+
+    def _args(self, lo: int, hi: int, slot: int) -> P2PArgs:
+        a = P2PArgs()
+        a.out = self.out.data_ptr() + lo * 4
+        for r in range(self.world):
+            a.inp[r] = self.in_ptr[r] + lo * 4
+            a.flags_peer[r] = self.flag_ptr[r]
+        a.flags_local = self.flags.data_ptr()
+        a.epoch = self.epoch.data_ptr()
+        a.err = self.err.data_ptr()
+        a.n = hi - lo
+        a.world, a.rank, a.slot = self.world, self.rank, slot
+        return a
+
+    @staticmethod
+    def _stream():
+        return torch.cuda.current_stream().cuda_stream
+
+    def begin_step(self):
+        """Before this step writes the gradient buffer: every peer finished reading it."""
+        a = self._args(0, 4, 0)
+        _lib.check(self.L.drn_p2p_wait(ctypes.byref(a), ctypes.c_void_p(self.epoch.data_ptr()), self._stream()),
+                   "drn_p2p_wait")
+
+    def reduce_bucket(self, i: int, lo: int, hi: int):
+        """Bucket i = grad[lo:hi] is complete on the current stream: publish it (compute stream)
+        and reduce it on the comm stream, whose kernel polls for the peers without blocking the
+        rest of this rank's backward pass."""
+        assert (hi - lo) % 4 == 0 and lo % 4 == 0 and i + 1 < N_SLOTS
+        a = self._args(lo, hi, i + 1)
+        cur = torch.cuda.current_stream()
+        _lib.check(self.L.drn_p2p_signal(ctypes.byref(a), 0, cur.cuda_stream), "drn_p2p_signal")
+        self.comm.wait_stream(cur)
+        # at most 128 workgroups: a reduce waiting for a slow peer must leave most CUs to this
+        # rank's own backward kernels (which publish the later buckets the peers wait for)
+        blocks = max(1, min(128, (hi - lo) // 4 // 256))
+        _lib.check(self.L.drn_p2p_reduce(ctypes.byref(a), blocks, self.comm.cuda_stream), "drn_p2p_reduce")
+
+    def end_step(self):
+        """All buckets reduced on this rank: tell the peers their inputs are free, and order the
+        compute stream after the reductions."""
+        a = self._args(0, 4, 0)
+        _lib.check(self.L.drn_p2p_signal(ctypes.byref(a), 1, self.comm.cuda_stream), "drn_p2p_signal")
+        torch.cuda.current_stream().wait_stream(self.comm)
+
+    def check(self):
+        """Raise if a device-side wait timed out (a peer never arrived)."""
+        e = int(self.err.item())
+        if e:
+            raise RuntimeError(f"P2P all-reduce timed out waiting for peers (code {e})")
+
+    def close(self):
+        h = _hip()
+        for p in self._opened:
+            h.hipIpcCloseMemHandle(ctypes.c_void_p(p))
+        self._opened = []

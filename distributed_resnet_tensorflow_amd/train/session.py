@@ -34,7 +34,7 @@ def make_backend(device: str):
 class TrainingSession:
     def __init__(self, spec, batch: int, cluster, *, weight_decay: float, lr_schedule, checkpoint_dir: str = "",
                  max_to_keep: int = 5, seed: int = 0, use_graph: bool = True, sync_mode: str = "sync",
-                 bucket_mb: float = 25.0, meta: Optional[dict] = None):
+                 bucket_mb: float = 25.0, meta: Optional[dict] = None, allreduce: str = "rccl"):
         self.cluster = cluster
         self.spec = spec
         self.device = torch.device(cluster.device)
@@ -42,7 +42,8 @@ class TrainingSession:
         self.ex = Executor(spec, batch, self.be, self.device, seed=seed, weight_decay=weight_decay)
         self.lr = lr_schedule
         self.meta = meta or {}
-        self.engine = DataParallelEngine(self.ex, bucket_mb=bucket_mb, mode=sync_mode) if cluster.distributed else None
+        self.engine = DataParallelEngine(self.ex, bucket_mb=bucket_mb, mode=sync_mode,
+                                         allreduce=allreduce) if cluster.distributed else None
         self.world = cluster.world
         self.ckpt_dir = checkpoint_dir
         self.saver = Saver(checkpoint_dir, max_to_keep) if (checkpoint_dir and cluster.is_chief) else None

@@ -35,7 +35,7 @@ def _make(spec, N, shard, seed):
     return ex
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, allreduce="rccl"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         torch.cuda.set_device(0)
@@ -44,8 +44,9 @@ def _worker(rank, world, port, q):
         from distributed_resnet_tensorflow_amd.parallel.engine import DataParallelEngine
         spec, N = cifar_resnet_v2(8), 8
         ex = _make(spec, N, rank, seed=1 + rank)
-        eng = DataParallelEngine(ex, bucket_mb=0.05)
+        eng = DataParallelEngine(ex, bucket_mb=0.05, allreduce=allreduce)
         assert len(eng.buckets) > 1
+        assert (eng.p2p is not None) == (allreduce == "p2p")
         eng.broadcast_parameters()
         exp = torch.zeros_like(ex.P.grad)
         for r in range(world):
@@ -53,11 +54,14 @@ def _worker(rank, world, port, q):
             e2.forward(True)
             e2.backward()
             exp += e2.P.grad / world
-        ex.forward(True)
-        eng.begin_step()
-        ex.backward()
-        g = eng.finish()
+        for _ in range(3 if allreduce == "p2p" else 1):   # p2p: exercise the epoch protocol
+            ex.forward(True)
+            eng.begin_step()
+            ex.backward()
+            g = eng.finish()
         torch.cuda.synchronize()
+        if eng.p2p is not None:
+            eng.p2p.check()
         err = ((g / world - exp).norm() / exp.norm()).item()
         ex.set_lr(0.1)
         ex.apply_gradients(grad_scale=1.0 / world, grad=g)
@@ -74,11 +78,14 @@ def _worker(rank, world, port, q):
         q.put((rank, repr(e) + traceback.format_exc(), False))
 
 
-def test_dp_engine_gpu_two_ranks_one_device():
+@pytest.mark.parametrize("allreduce", ["rccl", "p2p"])
+def test_dp_engine_gpu_two_ranks_one_device(allreduce):
+    """rccl here means the engine's torch.distributed path (gloo on this one-GPU box); p2p is
+    the one-shot HIP-IPC kernel path (parallel/p2p.py) with its device-side epoch flags."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q, allreduce)) for r in range(2)]
     for p in ps:
         p.start()
     res = [q.get(timeout=300) for _ in ps]
