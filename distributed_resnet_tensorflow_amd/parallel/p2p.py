@@ -26,7 +26,16 @@ _HIP = None
 
 
 class _IpcHandle(ctypes.Structure):
-    _fields_ = [("reserved", ctypes.c_char * 64)]
+    _fields_ = [("reserved", ctypes.c_uint8 * 64)]  # c_uint8, not c_char: handles contain NUL bytes
+
+    @classmethod
+    def from_bytes(cls, b: bytes) -> "_IpcHandle":
+        h = cls()
+        ctypes.memmove(ctypes.addressof(h), b, 64)
+        return h
+
+    def to_bytes(self) -> bytes:
+        return ctypes.string_at(ctypes.addressof(self), 64)
 
 
 class P2PArgs(ctypes.Structure):
@@ -70,7 +79,7 @@ def _export(t: torch.Tensor):
            "hipMemGetAddressRange")
     handle = _IpcHandle()
     _check(h.hipIpcGetMemHandle(ctypes.byref(handle), base), "hipIpcGetMemHandle")
-    return bytes(handle.reserved), t.data_ptr() - base.value
+    return handle.to_bytes(), t.data_ptr() - base.value
 
 
 class P2PAllReduce:
@@ -106,8 +115,7 @@ class P2PAllReduce:
                 continue
             ptrs = []
             for hb, off in ((gh, goff), (fh, foff)):
-                hd = _IpcHandle()
-                hd.reserved = hb
+                hd = _IpcHandle.from_bytes(hb)
                 p = ctypes.c_void_p()
                 _check(h.hipIpcOpenMemHandle(ctypes.byref(p), hd, 1), "hipIpcOpenMemHandle")  # lazy peer access
                 self._opened.append(p.value)
