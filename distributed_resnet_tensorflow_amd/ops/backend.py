@@ -233,10 +233,15 @@ class HipBackend(_Common):
         mean, invstd)) the fused BN-backward reduction with ReLU-masked output."""
         self.launch_conv(self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd))
 
+    WGRAD_TARGET_BLOCKS = int(os.environ.get("DRN_WGRAD_TARGET_BLOCKS", "512"))  # measured: 512 > 384, 640, 1024
+    WGRAD_MIN_STEPS = int(os.environ.get("DRN_WGRAD_MIN_STEPS", "8"))
+
     @staticmethod
-    def wgrad_splits(M, Ktot, K, target_blocks: int = 640, min_steps: int = 8):
+    def wgrad_splits(M, Ktot, K, target_blocks: int = 0, min_steps: int = 0):
         """Split-K over output pixels: enough workgroups to fill 256 CUs (~2.5 per CU) while
         keeping >= min_steps 64-pixel steps per split so partial slabs stay cheap."""
+        target_blocks = target_blocks or HipBackend.WGRAD_TARGET_BLOCKS
+        min_steps = min_steps or HipBackend.WGRAD_MIN_STEPS
         bkk = 128 if Ktot > 64 else 64
         bco = 128 if K > 64 else 64
         tiles = ((Ktot + bkk - 1) // bkk) * ((K + bco - 1) // bco)

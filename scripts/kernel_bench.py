@@ -86,7 +86,7 @@ def main():
         if a.sweep:
             from distributed_resnet_tensorflow_amd.ops.backend import dgrad_geom as _dg
             res_f, res_d = [], []
-            for cfg in [100] + list(range(8)):
+            for cfg in [100] + list(range(be.L.drn_conv_glds_num_cfgs())):
                 af = be.conv_args(x, w, y, g, in_bn=pro, stats=st)
                 af.cfg = cfg
                 res_f.append((timeit(lambda: be.launch_conv(af), a.iters), cfg))
