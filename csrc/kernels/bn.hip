@@ -18,6 +18,7 @@
 // fp32 atomics make the statistics order-nondeterministic in the last bits (like cuDNN's).
 // Every kernel reads/writes 16-byte vectors (8 channels) per lane.
 #include "drn_common.h"
+#include <stdlib.h>
 
 namespace drn {
 
@@ -430,9 +431,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_stats_kernel(
   }
 }
 
+static int g_apply_grid_cap = 0;
 static inline int grid_for(int64_t nvec) {
+  if (g_apply_grid_cap == 0) {
+    const char* e = getenv("DRN_BN_APPLY_GRID");
+    g_apply_grid_cap = e ? atoi(e) : 2048;  // measured: 2048 < 4096 < 8192 < 16384 workgroups
+    if (g_apply_grid_cap < 1) g_apply_grid_cap = 8192;
+  }
   int64_t b = (nvec + 255) / 256;
-  if (b > 8192) b = 8192;
+  if (b > g_apply_grid_cap) b = g_apply_grid_cap;
   if (b < 1) b = 1;
   return (int)b;
 }

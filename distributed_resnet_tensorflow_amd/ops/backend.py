@@ -121,9 +121,9 @@ class HipBackend(_Common):
     name = "hip"
     act_dtype = torch.bfloat16
     acc_dtype = torch.float32
-    # replicas of every BN statistics accumulator: producer block b adds into replica b % 32,
+    # replicas of every BN statistics accumulator: producer block b adds into replica b % R,
     # the finalize kernels sum them (same-address fp32 atomics serialize at ~15 ns each)
-    stats_replicas = 32
+    stats_replicas = int(os.environ.get("DRN_STATS_REPLICAS", "8"))  # measured: 8 ~ 4 < 16 < 32 < 64
 
     def __init__(self, device="cuda"):
         self.device = torch.device(device)
@@ -331,7 +331,7 @@ class HipBackend(_Common):
     @staticmethod
     def bn_rows_per_block(M, C):
         rpp = max(1, 256 // (C // 8))
-        G_target = 512
+        G_target = int(os.environ.get("DRN_BN_BLOCKS", "512"))
         rpb = max(rpp, ((M + G_target - 1) // G_target + rpp - 1) // rpp * rpp)
         return rpb
 
