@@ -30,19 +30,23 @@ namespace drn {
 // epi_prefetch() computes those output offsets and issues the 16-byte loads of the residual
 // and of the fused-BN-backward input BEFORE the main loop, so their latency hides behind the
 // MFMA work instead of stalling the epilogue (short-K launches are otherwise dominated by it).
-template <int BP, int BC, int NT = 256>
+// PF = false: nothing is prefetched (no residual / BN-backward operand; saves the 64 VGPRs
+// that would otherwise cap the occupancy).
+template <int BP, int BC, int NT = 256, bool PF = true>
 struct EpiPre {
   static constexpr int CHR = BC / 8;  // output 16-byte chunks per pixel row
   static constexpr int RPI = NT / CHR;
   static constexpr int IT = BP / RPI;
+  static constexpr int NPF = PF ? IT : 1;
   int off[IT];     // element offset of the chunk, -1 when outside the output
-  uint4 res[IT];
-  uint4 bx[IT];
+  uint4 res[NPF];
+  uint4 bx[NPF];
 };
 
-template <int BP, int BC, int NT = 256>
-__device__ __forceinline__ void epi_prefetch(const DrnConvFwdArgs& a, int m0, int c0, int M, EpiPre<BP, BC, NT>& e) {
-  using E = EpiPre<BP, BC, NT>;
+template <int BP, int BC, int NT = 256, bool PF = true>
+__device__ __forceinline__ void epi_prefetch(const DrnConvFwdArgs& a, int m0, int c0, int M,
+                                             EpiPre<BP, BC, NT, PF>& e) {
+  using E = EpiPre<BP, BC, NT, PF>;
   const int tid = threadIdx.x;
   const int ch = tid % E::CHR;
   const int c = c0 + ch * 8;
@@ -66,8 +70,10 @@ __device__ __forceinline__ void epi_prefetch(const DrnConvFwdArgs& a, int m0, in
       }
     }
     e.off[it] = off;
-    e.res[it] = (res && off >= 0) ? *reinterpret_cast<const uint4*>(res + off) : make_uint4(0u, 0u, 0u, 0u);
-    e.bx[it] = (bx && off >= 0) ? *reinterpret_cast<const uint4*>(bx + off) : make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (PF) {
+      e.res[it] = (res && off >= 0) ? *reinterpret_cast<const uint4*>(res + off) : make_uint4(0u, 0u, 0u, 0u);
+      e.bx[it] = (bx && off >= 0) ? *reinterpret_cast<const uint4*>(bx + off) : make_uint4(0u, 0u, 0u, 0u);
+    }
   }
 }
 
@@ -76,10 +82,10 @@ __device__ __forceinline__ void epi_prefetch(const DrnConvFwdArgs& a, int m0, in
 // written as whole 2*BC-byte pixel rows per wave instruction (fully coalesced). Optional
 // residual add, optional strided output map, optional per-channel sum/sumsq for the next BN,
 // or (bn_x set) the fused BN-backward reduction with ReLU-masked output.
-template <int BP, int BC, int WP, int WC, int MI, int MJ, int NT = 256>
+template <int BP, int BC, int WP, int WC, int MI, int MJ, int NT = 256, bool PF = true>
 __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* smem, f32x4_t (&acc)[MI][MJ], int wp,
-                                              int wc, int m0, int c0, int M, const EpiPre<BP, BC, NT>& e) {
-  using E = EpiPre<BP, BC, NT>;
+                                              int wc, int m0, int c0, int M, const EpiPre<BP, BC, NT, PF>& e) {
+  using E = EpiPre<BP, BC, NT, PF>;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   constexpr int CF = BC / 4;   // fp32 16-byte chunks per staged row
@@ -126,7 +132,8 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
       float f[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       if (has_res) {
         float r8[8];
-        unpack8(e.res[it], r8);
+        if constexpr (PF) unpack8(e.res[it], r8);
+        else unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(a.residual) + off), r8);
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] += r8[j];
       }
@@ -136,7 +143,8 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
       if (bnb) {
         // BN-backward: mask by the forward ReLU, accumulate sum g and sum g * xhat
         float xb[8];
-        unpack8(e.bx[it], xb);
+        if constexpr (PF) unpack8(e.bx[it], xb);
+        else unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(a.bn_x) + off), xb);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float g = (xb[j] * bsc[j] + bsh[j] > 0.f) ? q8[j] : 0.f;
@@ -411,7 +419,7 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BP, int BC, int WAVES_P, int NS, int NW = 4>
+template <int BP, int BC, int WAVES_P, int NS, int NW = 4, bool PF = true>
 __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a, const void* __restrict__ zero) {
   constexpr int NT = NW * 64;
   constexpr int WAVES_C = NW / WAVES_P;
@@ -520,8 +528,8 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   const int swz = (fr >> 1) & 7;  // rows of a fragment group are 16-aligned: bits 1..3 = fr's
 
   const int T = Ktot / 64;
-  EpiPre<BP, BC, NT> epre;
-  epi_prefetch<BP, BC, NT>(a, m0, c0, M, epre);  // residual / BN inputs in flight during the main loop
+  EpiPre<BP, BC, NT, PF> epre;
+  epi_prefetch<BP, BC, NT, PF>(a, m0, c0, M, epre);  // residual / BN inputs in flight during the main loop
 #pragma unroll
   for (int s = 0; s < D; ++s)
     if (s < T) issue(s);
@@ -552,15 +560,15 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   }
   __syncthreads();  // all fragment reads done before the epilogue reuses the LDS
   // (the launcher sizes the dynamic LDS for max(NS * STAGE, BP * BC * 4))
-  conv_epilogue<BP, BC, WP, WC, MI, MJ, NT>(a, smem, acc, wp, wc, m0, c0, M, epre);
+  conv_epilogue<BP, BC, WP, WC, MI, MJ, NT, PF>(a, smem, acc, wp, wc, m0, c0, M, epre);
 }
 
-template <int BP, int BC, int WAVES_P, int NS, int NW = 4>
-static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
+template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF>
+static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
   constexpr int LDS0 = NS * (BC + BP) * 128;
   constexpr int LDS = LDS0 > BP * BC * 4 ? LDS0 : BP * BC * 4;  // epilogue staging tile
   static bool attr_set = false;
-  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS, NW>;
+  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS, NW, PF>;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
@@ -571,6 +579,14 @@ static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t str
   a->tiles_p = tiles_p;
   hipLaunchKernelGGL(kern, dim3(tiles_p * tiles_c), dim3(NW * 64), LDS, stream, *a, zero);
   return (int)hipGetLastError();
+}
+
+// epilogue operands (residual / BN-backward input) are prefetched only when present
+template <int BP, int BC, int WAVES_P, int NS, int NW = 4>
+static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
+  if (a->residual != nullptr || a->bn_x != nullptr)
+    return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true>(a, zero, stream);
+  return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false>(a, zero, stream);
 }
 
 // Tile configurations of the LDS-DMA kernel (index = DRN conv config id, also used by the
@@ -587,7 +603,10 @@ static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t str
   X(8, 256, 128, 4, 2, 8)    \
   X(9, 256, 128, 4, 3, 8)    \
   X(10, 128, 256, 2, 2, 8)   \
-  X(11, 128, 256, 2, 3, 8)
+  X(11, 128, 256, 2, 3, 8)   \
+  X(12, 128, 64, 2, 2, 4)    \
+  X(13, 64, 128, 1, 2, 4)    \
+  X(14, 64, 64, 2, 2, 4)
 
 static int launch_glds_cfg(int cfg, DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
   switch (cfg) {
@@ -674,7 +693,7 @@ DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
 }
 
 DRN_API int drn_conv_glds_cfg_bp(int cfg) { return drn::glds_cfg_bp(cfg); }
-DRN_API int drn_conv_glds_num_cfgs() { return 12; }
+DRN_API int drn_conv_glds_num_cfgs() { return 15; }
 DRN_API int drn_conv_glds_default_cfg(const DrnConvFwdArgs* a) { return drn::glds_default_cfg(a); }
 
 DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s) {
