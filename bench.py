@@ -150,6 +150,9 @@ def main():
             "final_loss": round(loss, 4),
         }
         print(json.dumps(out), flush=True)
+    if os.environ.get("DRN_PRINT_TUNE") == "1" and rank == 0:
+        for key, cfg, us in be.tune_log:
+            print(f"[tune] {key} -> {cfg} ({us} us)", file=sys.stderr)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

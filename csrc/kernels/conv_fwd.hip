@@ -174,8 +174,8 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
       red[tid * 16 + 8 + j] = ssq[j];
     }
     __syncthreads();
-    if (tid < 2 * BC) {
-      const int cl = tid >> 1, which = tid & 1;
+    for (int t = tid; t < 2 * BC; t += NT) {  // 2*BC may exceed the thread count (BC = 256)
+      const int cl = t >> 1, which = t & 1;
       const int chh = cl >> 3, j = cl & 7;
       float s = 0.f;
       for (int t2 = chh; t2 < NT; t2 += CHR) s += red[t2 * 16 + which * 8 + j];
@@ -606,7 +606,9 @@ static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t str
   X(11, 128, 256, 2, 3, 8)   \
   X(12, 128, 64, 2, 2, 4)    \
   X(13, 64, 128, 1, 2, 4)    \
-  X(14, 64, 64, 2, 2, 4)
+  X(14, 64, 64, 2, 2, 4)     \
+  X(15, 64, 256, 1, 2, 4)    \
+  X(16, 32, 128, 1, 2, 4)
 
 static int launch_glds_cfg(int cfg, DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
   switch (cfg) {
@@ -693,7 +695,7 @@ DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
 }
 
 DRN_API int drn_conv_glds_cfg_bp(int cfg) { return drn::glds_cfg_bp(cfg); }
-DRN_API int drn_conv_glds_num_cfgs() { return 15; }
+DRN_API int drn_conv_glds_num_cfgs() { return 17; }
 DRN_API int drn_conv_glds_default_cfg(const DrnConvFwdArgs* a) { return drn::glds_default_cfg(a); }
 
 DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s) {

@@ -181,7 +181,8 @@ class HipBackend(_Common):
     @staticmethod
     def conv_key(a) -> tuple:
         return (a.N, a.H, a.W, a.C, a.K, a.R, a.S, a.P, a.Q, a.stride, a.pad_h, a.pad_w, a.dil,
-                a.in_scale is not None, a.out_stride)
+                a.in_scale is not None, a.out_stride, a.residual is not None, a.bn_x is not None,
+                a.stats is not None)
 
     def launch_conv(self, a):
         if a.cfg == -1 and self.autotune and self.forced_cfg is None:

@@ -82,7 +82,7 @@ GLDS_CASES = [
 
 
 @pytest.mark.parametrize("case", GLDS_CASES)
-@pytest.mark.parametrize("cfg", list(range(15)))
+@pytest.mark.parametrize("cfg", list(range(17)))
 def test_conv_fwd_glds_configs(hip, ref, case, cfg):
     """Every tile/pipeline configuration of the LDS-DMA conv kernel vs the fp32 reference,
     with residual add + BN statistics epilogue."""
@@ -118,7 +118,7 @@ def test_conv_glds_out_map(hip, ref):
     om = OutMap(P=P, Q=P, stride=2, oh=1, ow=0)
     y_ref = torch.zeros(N, 2 * P, 2 * P, K)
     ref.conv_fwd(x.float(), w.float(), y_ref, ConvGeom(1, 0, 0), out_map=om)
-    for cfg in range(15):
+    for cfg in range(17):
         y = torch.zeros(N, 2 * P, 2 * P, K, dtype=torch.bfloat16, device="cuda")
         a = hip.conv_args(x.cuda(), w.cuda(), y, ConvGeom(1, 0, 0), out_map=om)
         a.cfg = cfg
