@@ -309,9 +309,10 @@ __device__ __forceinline__ void lgkm_fence(s16x4v (&a)[MI][2], s16x4v (&b)[MJ][2
   for (int j = 0; j < MJ; ++j) asm volatile("" : "+v"(b[j][0]), "+v"(b[j][1]));
 }
 
-template <int BKK, int BCO, int NS>
+template <int BKK, int BCO, int NS, int BP = 64>
 __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a, const void* __restrict__ zero) {
-  constexpr int BP = 64;
+  static_assert(BP == 32 || BP == 64, "pixels per stage");
+  constexpr int KS = BP / 32;  // 32-deep MFMA k-slices per stage
   constexpr int WA = BKK * 2, WB = BCO * 2;       // image row bytes
   constexpr int A_BYTES = BP * WA;
   constexpr int STAGE = A_BYTES + BP * WB;
@@ -458,9 +459,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
     for (int i = 0; i < MI; ++i) ba[i] = cur + a_lane[i];
 #pragma unroll
     for (int j = 0; j < MJ; ++j) bb[j] = cur + b_lane[j];
-    s16x4v fa[2][MI][2], fb[2][MJ][2];
-    static_for<0, 2>([&](auto KS) {
-      constexpr int ks = decltype(KS)::value;
+    s16x4v fa[KS][MI][2], fb[KS][MJ][2];
+    static_for<0, KS>([&](auto KSI) {
+      constexpr int ks = decltype(KSI)::value;
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         fa[ks][i][0] = tr_read_asm<(32 * ks) * WA>(ba[i]);
@@ -473,9 +474,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
       }
     });
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      if (ks == 0) lgkm_fence<(2 * (MI + MJ) > 15 ? 15 : 2 * (MI + MJ))>(fa[0], fb[0]);  // 4-bit counter
-      else lgkm_fence<0>(fa[1], fb[1]);
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) lgkm_fence<(2 * (MI + MJ) > 15 ? 15 : 2 * (MI + MJ))>(fa[ks], fb[ks]);  // 4-bit counter
+      else lgkm_fence<0>(fa[ks], fb[ks]);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -501,11 +502,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
     }
 }
 
-template <int BKK, int BCO, int NS>
+template <int BKK, int BCO, int NS, int BP = 64>
 static int launch_wgrad_glds(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
-  constexpr int LDS = NS * (64 * BKK * 2 + 64 * BCO * 2);
+  constexpr int LDS = NS * (BP * BKK * 2 + BP * BCO * 2);
   static bool attr_set = false;
-  auto kern = conv_wgrad_glds_kernel<BKK, BCO, NS>;
+  auto kern = conv_wgrad_glds_kernel<BKK, BCO, NS, BP>;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
@@ -517,20 +518,27 @@ static int launch_wgrad_glds(DrnConvWgradArgs* a, const void* zero, hipStream_t 
   return (int)hipGetLastError();
 }
 
-static int dispatch_wgrad_glds(DrnConvWgradArgs* a, const void* zero, int ns, hipStream_t s) {
+template <int NS, int BP>
+static int dispatch_wgrad_tile(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
   const int Ktot = a->R * a->S * a->C;
   const bool wide_k = Ktot > 64;
   const bool wide_c = a->K > 64;
-  if (ns == 3) {
-    if (wide_k && wide_c) return launch_wgrad_glds<128, 128, 3>(a, zero, s);
-    if (wide_k) return launch_wgrad_glds<128, 64, 3>(a, zero, s);
-    if (wide_c) return launch_wgrad_glds<64, 128, 3>(a, zero, s);
-    return launch_wgrad_glds<64, 64, 3>(a, zero, s);
+  if (wide_k && wide_c) return launch_wgrad_glds<128, 128, NS, BP>(a, zero, s);
+  if (wide_k) return launch_wgrad_glds<128, 64, NS, BP>(a, zero, s);
+  if (wide_c) return launch_wgrad_glds<64, 128, NS, BP>(a, zero, s);
+  return launch_wgrad_glds<64, 64, NS, BP>(a, zero, s);
+}
+
+// pipeline id: 2 / 3 = 2 / 3 stages of 64 pixels; 4 / 5 / 6 = 2 / 3 / 4 stages of 32 pixels
+// (half the LDS per stage: more resident workgroups per CU)
+static int dispatch_wgrad_glds(DrnConvWgradArgs* a, const void* zero, int ns, hipStream_t s) {
+  switch (ns) {
+    case 3: return dispatch_wgrad_tile<3, 64>(a, zero, s);
+    case 4: return dispatch_wgrad_tile<2, 32>(a, zero, s);
+    case 5: return dispatch_wgrad_tile<3, 32>(a, zero, s);
+    case 6: return dispatch_wgrad_tile<4, 32>(a, zero, s);
+    default: return dispatch_wgrad_tile<2, 64>(a, zero, s);
   }
-  if (wide_k && wide_c) return launch_wgrad_glds<128, 128, 2>(a, zero, s);
-  if (wide_k) return launch_wgrad_glds<128, 64, 2>(a, zero, s);
-  if (wide_c) return launch_wgrad_glds<64, 128, 2>(a, zero, s);
-  return launch_wgrad_glds<64, 64, 2>(a, zero, s);
 }
 
 // out[i] (+)= scale * sum_k ws[k][i]: block = 64 float4 columns x 4 split-groups; every

@@ -214,7 +214,9 @@ class HipBackend(_Common):
         best, best_t = 100, float("inf")
         s = self.stream()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        for cfg in [100] + list(range(self.L.drn_conv_glds_num_cfgs())):
+        cands = os.environ.get("DRN_CONV_CANDS")
+        cands = [int(c) for c in cands.split(",")] if cands else [100] + list(range(self.L.drn_conv_glds_num_cfgs()))
+        for cfg in cands:
             t.cfg = cfg
             for _ in range(2):
                 _lib.check(self.L.drn_conv_fwd2(ctypes.byref(t), self.zero_page.data_ptr(), s), "drn_conv_fwd")
@@ -290,14 +292,16 @@ class HipBackend(_Common):
         _lib.check(self.L.drn_conv_wgrad2(ctypes.byref(a), self.zero_page.data_ptr(), ns, st), "drn_conv_wgrad")
 
     def _tune_wgrad(self, a, key, iters: int = 5) -> int:
-        """Pick the wgrad pipeline (0: register-staged, 2/3: LDS-DMA stages) by timing; the
+        """Pick the wgrad pipeline (0: register-staged, 2/3: LDS-DMA stages of 64 pixels, 4/5/6:
+        2/3/4 stages of 32 pixels) by timing; the
         kernel only writes the split-K workspace (or the gradient slot, rewritten right after)."""
         if a.in_scale is not None:
             return 0
         st = self.stream()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         best, best_t = 2, float("inf")
-        for ns in (0, 2, 3):
+        cands = tuple(int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6").split(","))
+        for ns in cands:
             for _ in range(2):
                 self._wgrad_kernel(a, ns, st)
             ev0.record()

@@ -211,7 +211,7 @@ WGRAD_GLDS_CASES = [
 
 
 @pytest.mark.parametrize("case", WGRAD_GLDS_CASES)
-@pytest.mark.parametrize("ns", [0, 2, 3])
+@pytest.mark.parametrize("ns", [0, 2, 3, 4, 5, 6])
 def test_conv_wgrad_pipelines(hip, ref, case, ns):
     """Register-staged (ns=0) and LDS-DMA (2/3 stages) weight-gradient kernels vs fp32."""
     N, H, W, C, K, R, s, p = case
