@@ -419,19 +419,32 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BP, int BC, int WAVES_P, int NS, int NW = 4, bool PF = true>
+// BK = 64: 128-byte LDS rows, slot(chunk c of row r) = c ^ ((r >> 1) & 7)
+// BK = 32: 64-byte LDS rows (a stage holds one 32-deep MFMA k-slice; twice the stages in the same
+//          LDS, i.e. a deeper pipeline), slot = c ^ (((r >> 2) & 1) << 1); both conflict-free for
+//          the ds_read_b128 fragment reads (exhaustive check over the gfx950 lane groups).
+template <int BK>
+__device__ __forceinline__ int glds_swz(int row) {
+  if constexpr (BK == 64) return (row >> 1) & 7;
+  return ((row >> 2) & 1) << 1;
+}
+
+template <int BP, int BC, int WAVES_P, int NS, int NW = 4, bool PF = true, int BK = 64>
 __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a, const void* __restrict__ zero) {
+  static_assert(BK == 64 || BK == 32, "k per stage");
   constexpr int NT = NW * 64;
   constexpr int WAVES_C = NW / WAVES_P;
   constexpr int WP = BP / WAVES_P, WC = BC / WAVES_C;
   constexpr int MI = WC / 16, MJ = WP / 16;
-  constexpr int ROWB = 128;                 // 64 bf16 of k per LDS row
+  constexpr int ROWB = BK * 2;              // bytes of one LDS row (BK bf16 of k)
+  constexpr int CPR = BK / 8;               // 16-byte chunks per row
+  constexpr int RPG = 1024 / ROWB;          // rows per glds wave-instruction (1 KiB)
   constexpr int STAGE = (BC + BP) * ROWB;
-  constexpr int GA = BC / (8 * NW), GB = BP / (8 * NW);  // glds wave-instructions per stage (8 rows each)
+  constexpr int GA = BC / (RPG * NW), GB = BP / (RPG * NW);  // glds wave-instructions per stage
   constexpr int G = GA + GB;
   constexpr int D = NS - 1;                 // stages in flight ahead of the computing one
   static_assert(WAVES_P * WAVES_C == NW && MI >= 1 && MJ >= 1, "wave layout");
-  static_assert(GA * 8 * NW == BC && GB * 8 * NW == BP, "rows must split evenly over the waves");
+  static_assert(GA * RPG * NW == BC && GB * RPG * NW == BP, "rows must split evenly over the waves");
   static_assert(NS >= 2 && G * (D > 1 ? D - 1 : 1) < 64, "pipeline depth");
 
   extern __shared__ __attribute__((aligned(1024))) char smem[];
@@ -450,21 +463,22 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   const int c0 = tc * BC;
 
   // ---- per-lane loader state ----
-  const int lrow = lane >> 3;
+  const int lrow = lane / CPR;
+  const int lpc = lane % CPR;
   const bf16_t* __restrict__ xg = reinterpret_cast<const bf16_t*>(a.x);
   const bf16_t* wsrc[GA];
 #pragma unroll
   for (int i = 0; i < GA; ++i) {
-    const int row = 8 * NW * i + 8 * wave + lrow;
-    const int lc = (lane & 7) ^ ((row >> 1) & 7);
+    const int row = RPG * NW * i + RPG * wave + lrow;
+    const int lc = lpc ^ glds_swz<BK>(row);
     const int c = c0 + row;
     wsrc[i] = c < a.K ? reinterpret_cast<const bf16_t*>(a.w) + (size_t)c * Ktot + lc * 8 : nullptr;
   }
   int boff[GB], bh[GB], bw[GB];
 #pragma unroll
   for (int i = 0; i < GB; ++i) {
-    const int row = 8 * NW * i + 8 * wave + lrow;
-    const int lc = (lane & 7) ^ ((row >> 1) & 7);  // (BC + row) has the same bits 1..3
+    const int row = RPG * NW * i + RPG * wave + lrow;
+    const int lc = lpc ^ glds_swz<BK>(row);  // (BC + row) has the same swizzle bits
     const int m = m0 + row;
     if (m < M) {
       const int pq = a.P * a.Q;
@@ -489,7 +503,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
       const void* src = wsrc[i] ? (const void*)(wsrc[i] + ik) : zero;
-      glds16(src, st + (8 * NW * i + 8 * wave) * ROWB);
+      glds16(src, st + (RPG * NW * i + RPG * wave) * ROWB);
     }
     const int tap_off = (ir * a.W + is) * C + ici;
 #pragma unroll
@@ -497,10 +511,10 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
       const int h = bh[i] + ir, w = bw[i] + is;
       const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
       const void* src = ok ? (const void*)(xg + (boff[i] + tap_off)) : zero;
-      glds16(src, st + (BC + 8 * NW * i + 8 * wave) * ROWB);
+      glds16(src, st + (BC + RPG * NW * i + RPG * wave) * ROWB);
     }
-    ik += 64;
-    ici += 64;
+    ik += BK;
+    ici += BK;
     if (ici == C) {
       ici = 0;
       if (++is == a.S) {
@@ -525,9 +539,9 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   for (int i = 0; i < MI; ++i) aoff[i] = (wc * WC + i * 16 + fr) * ROWB;
 #pragma unroll
   for (int j = 0; j < MJ; ++j) boffl[j] = (BC + wp * WP + j * 16 + fr) * ROWB;
-  const int swz = (fr >> 1) & 7;  // rows of a fragment group are 16-aligned: bits 1..3 = fr's
+  const int swz = glds_swz<BK>(fr);  // fragment row groups are 16-aligned: the swizzle bits are fr's
 
-  const int T = Ktot / 64;
+  const int T = Ktot / BK;
   EpiPre<BP, BC, NT, PF> epre;
   epi_prefetch<BP, BC, NT, PF>(a, m0, c0, M, epre);  // residual / BN inputs in flight during the main loop
 #pragma unroll
@@ -543,7 +557,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
     if (t + D < T) issue((t + D) % NS);
     const char* st = smem + (t % NS) * STAGE;
 #pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
+    for (int kh = 0; kh < BK / 32; ++kh) {
       const int slot = ((kh * 4 + fk) ^ swz) * 16;
       bf16x8_t af[MI], bfr[MJ];
 #pragma unroll
@@ -563,12 +577,12 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   conv_epilogue<BP, BC, WP, WC, MI, MJ, NT, PF>(a, smem, acc, wp, wc, m0, c0, M, epre);
 }
 
-template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF>
+template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF, int BK>
 static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
-  constexpr int LDS0 = NS * (BC + BP) * 128;
+  constexpr int LDS0 = NS * (BC + BP) * BK * 2;
   constexpr int LDS = LDS0 > BP * BC * 4 ? LDS0 : BP * BC * 4;  // epilogue staging tile
   static bool attr_set = false;
-  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS, NW, PF>;
+  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS, NW, PF, BK>;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
@@ -582,11 +596,12 @@ static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t 
 }
 
 // epilogue operands (residual / BN-backward input) are prefetched only when present
-template <int BP, int BC, int WAVES_P, int NS, int NW = 4>
+template <int BP, int BC, int WAVES_P, int NS, int NW = 4, int BK = 64>
 static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
+  if (a->C % BK) return (int)hipErrorInvalidValue;
   if (a->residual != nullptr || a->bn_x != nullptr)
-    return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true>(a, zero, stream);
-  return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false>(a, zero, stream);
+    return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK>(a, zero, stream);
+  return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK>(a, zero, stream);
 }
 
 // Tile configurations of the LDS-DMA kernel (index = DRN conv config id, also used by the
@@ -608,13 +623,19 @@ static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t str
   X(13, 64, 128, 1, 2, 4)    \
   X(14, 64, 64, 2, 2, 4)     \
   X(15, 64, 256, 1, 2, 4)    \
-  X(16, 32, 128, 1, 2, 4)
+  X(16, 32, 128, 1, 2, 4)    \
+  X(17, 128, 128, 2, 4, 4, 32) \
+  X(18, 64, 128, 1, 4, 4, 32)  \
+  X(19, 128, 64, 2, 4, 4, 32)  \
+  X(20, 128, 128, 2, 3, 4, 32) \
+  X(21, 64, 128, 1, 3, 4, 32)  \
+  X(22, 256, 64, 4, 4, 4, 32)
 
 static int launch_glds_cfg(int cfg, DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
   switch (cfg) {
-#define DRN_X(id, bp, bc, wpv, ns, nw) \
-  case id:                             \
-    return launch_conv_glds<bp, bc, wpv, ns, nw>(a, zero, s);
+#define DRN_X(id, bp, bc, wpv, ns, nw, ...) \
+  case id:                                  \
+    return launch_conv_glds<bp, bc, wpv, ns, nw __VA_OPT__(, ) __VA_ARGS__>(a, zero, s);
     DRN_GLDS_CONFIGS(DRN_X)
 #undef DRN_X
     default:
@@ -624,8 +645,8 @@ static int launch_glds_cfg(int cfg, DrnConvFwdArgs* a, const void* zero, hipStre
 
 static int glds_cfg_bp(int cfg) {
   switch (cfg) {
-#define DRN_X(id, bp, bc, wpv, ns, nw) \
-  case id:                             \
+#define DRN_X(id, bp, bc, wpv, ns, nw, ...) \
+  case id:                                  \
     return bp;
     DRN_GLDS_CONFIGS(DRN_X)
 #undef DRN_X
@@ -639,6 +660,7 @@ static int glds_cfg_bp(int cfg) {
 // 64 x 128 tiles once the 128 x 128 grid stops filling the chip.
 static int glds_default_cfg(const DrnConvFwdArgs* a) {
   const long M = (long)a->N * a->P * a->Q;
+  if (a->C % 64) return 18;  // 32-channel inputs: the 32-deep-stage family
   auto blocks = [&](int bp, int bc) { return ((M + bp - 1) / bp) * ((a->K + bc - 1) / bc); };
   if (a->K <= 64) return blocks(256, 64) >= 384 ? 3 : 7;
   if (blocks(128, 128) >= 384) return 0;
@@ -683,7 +705,7 @@ DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s);
 
 // Whether the LDS-DMA kernel family supports this convolution.
 DRN_API int drn_conv_glds_ok(const DrnConvFwdArgs* a) {
-  return a->C % 64 == 0 && a->dil == 1 && a->in_scale == nullptr;
+  return a->C % 32 == 0 && a->dil == 1 && a->in_scale == nullptr;
 }
 
 // Dispatch on a->cfg; zero = >= 16 bytes of device zeros (the LDS-DMA loader's padding source).
@@ -695,7 +717,7 @@ DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
 }
 
 DRN_API int drn_conv_glds_cfg_bp(int cfg) { return drn::glds_cfg_bp(cfg); }
-DRN_API int drn_conv_glds_num_cfgs() { return 17; }
+DRN_API int drn_conv_glds_num_cfgs() { return 23; }
 DRN_API int drn_conv_glds_default_cfg(const DrnConvFwdArgs* a) { return drn::glds_default_cfg(a); }
 
 DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s) {

@@ -218,7 +218,9 @@ class HipBackend(_Common):
         cands = [int(c) for c in cands.split(",")] if cands else [100] + list(range(self.L.drn_conv_glds_num_cfgs()))
         for cfg in cands:
             t.cfg = cfg
-            for _ in range(2):
+            if self.L.drn_conv_fwd2(ctypes.byref(t), self.zero_page.data_ptr(), s) != 0:
+                continue  # configuration not applicable to this geometry (e.g. C % 64 != 0)
+            for _ in range(1):
                 _lib.check(self.L.drn_conv_fwd2(ctypes.byref(t), self.zero_page.data_ptr(), s), "drn_conv_fwd")
             ev0.record()
             for _ in range(iters):

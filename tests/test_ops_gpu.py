@@ -3,6 +3,8 @@
 Inputs are rounded to bf16 once and fed to both sides; the reference then runs in fp32, so
 the difference is accumulation order + the bf16 rounding of the kernel output.
 """
+import ctypes
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -78,11 +80,12 @@ GLDS_CASES = [
     (2, 13, 13, 64, 128, 3, 2, 1),     # stride 2, odd size, padding
     (1, 6, 6, 192, 72, 3, 1, 1),       # K % BC != 0 (zero-page weight rows)
     (2, 8, 8, 256, 64, 1, 2, 0),
+    (2, 9, 9, 96, 64, 3, 1, 1),        # C % 64 != 0: only the 32-deep-stage configs apply
 ]
 
 
 @pytest.mark.parametrize("case", GLDS_CASES)
-@pytest.mark.parametrize("cfg", list(range(17)))
+@pytest.mark.parametrize("cfg", list(range(23)))
 def test_conv_fwd_glds_configs(hip, ref, case, cfg):
     """Every tile/pipeline configuration of the LDS-DMA conv kernel vs the fp32 reference,
     with residual add + BN statistics epilogue."""
@@ -101,6 +104,9 @@ def test_conv_fwd_glds_configs(hip, ref, case, cfg):
     a = hip.conv_args(x.cuda(), w.cuda(), y, g, residual=res.cuda(), stats=st)
     assert hip.L.drn_conv_glds_ok(a) == 1 and a.stats_rep == 3
     a.cfg = cfg
+    if C % 64 and cfg < 17:
+        assert hip.L.drn_conv_fwd2(ctypes.byref(a), hip.zero_page.data_ptr(), hip.stream()) != 0
+        return
     hip.launch_conv(a)
     torch.cuda.synchronize()
     assert rel(y, y_ref) < 1e-2
@@ -118,7 +124,7 @@ def test_conv_glds_out_map(hip, ref):
     om = OutMap(P=P, Q=P, stride=2, oh=1, ow=0)
     y_ref = torch.zeros(N, 2 * P, 2 * P, K)
     ref.conv_fwd(x.float(), w.float(), y_ref, ConvGeom(1, 0, 0), out_map=om)
-    for cfg in range(17):
+    for cfg in range(23):
         y = torch.zeros(N, 2 * P, 2 * P, K, dtype=torch.bfloat16, device="cuda")
         a = hip.conv_args(x.cuda(), w.cuda(), y, ConvGeom(1, 0, 0), out_map=om)
         a.cfg = cfg
