@@ -97,6 +97,9 @@ def main():
         else:
             ex.apply_gradients()
 
+    # kernel autotuning pass (one plain forward + backward) before any collective is in flight,
+    # so every rank times its candidate kernels on an otherwise idle GPU
+    ex.autotune()
     use_graph = args.graph if args.graph >= 0 else int(world == 1)
     run = step
     if use_graph:

@@ -564,6 +564,20 @@ class Executor:
             table = self.wt_table if self.is_hip else self.wt_table.cpu()
             self.be.weight_tflip(src, self.wt_flat, table, self.wt_n, self.wt_total)
 
+    def autotune(self):
+        """Run one forward + backward so the backend times and fixes its kernel configurations
+        (conv tile / pipeline choice per geometry) before graph capture or any collective; the
+        BN moving statistics and gradients are restored afterwards (no training side effects)."""
+        saved = self.P.bn_state.clone()
+        hook, self.grad_ready = self.grad_ready, None
+        self.forward(train=True)
+        self.backward()
+        self.grad_ready = hook
+        self.P.bn_state.copy_(saved)
+        self.P.grad.zero_()
+        if self.is_hip:
+            torch.cuda.synchronize()
+
     def train_step(self, lr: Optional[float] = None, grad_scale: float = 1.0, allreduce: Optional[Callable] = None):
         if lr is not None:
             self.set_lr(lr)

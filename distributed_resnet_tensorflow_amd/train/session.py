@@ -50,6 +50,8 @@ class TrainingSession:
         self.data_state = {}
         self.restored_from = None
         self._restore()
+        if self.device.type == "cuda":
+            self.ex.autotune()  # fix kernel configurations before any collective / graph capture
         self.use_graph = use_graph and self.device.type == "cuda" and not cluster.distributed
         self._graph: Optional[StepGraph] = None
         self._metrics_cache = None
