@@ -54,32 +54,67 @@ __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict_
 // Full flip (stride-1 data gradient): Ru=R, r0=R-1, dr=-1. Stride-2 data gradients use one
 // sub-kernel per output phase (taps of one parity, dr=-2), so no MFMA work is spent on the
 // zeros of a dilated dY.
+//
+// For one tap the map is a K x C -> C x K matrix transpose, so the kernel is a tiled transpose:
+// one workgroup per (descriptor, tap, 64-k tile, 64-c tile); rows of 64 c are read with 16-byte
+// coalesced loads into LDS, and rows of 64 k leave with 16-byte coalesced stores. (An
+// element-per-thread gather reads each 2-byte element from its own 32-byte sector.) The LDS row
+// pitch of 66 elements (33 dwords) spreads the column reads of a wave over distinct banks.
 struct TDesc {
   int64_t src, dst;       // element offsets into the flat bf16 weight buffers
-  int32_t K, R, S, C;     // source KRSC dims
+  int32_t K, R, S, C;     // source KRSC dims (K, C multiples of 8)
   int32_t Ru, Sv, r0, s0; // destination taps and first source tap
-  int32_t dr, ds, pad0, pad1;
-  int64_t begin;          // prefix sum of destination element counts (work partition)
+  int32_t dr, ds, tk, tc; // tap steps; 64-wide tile counts along K and C
+  int64_t begin;          // prefix sum of tile counts (Ru*Sv*tk*tc per descriptor)
 };
 
+constexpr int TF_T = 64, TF_PITCH = 66;
+
 __global__ __launch_bounds__(256) void weight_tflip_kernel(const bf16_t* __restrict__ w, bf16_t* __restrict__ wt,
-                                                           const TDesc* __restrict__ table, int ntab,
-                                                           int64_t total) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    // binary search the descriptor owning element i
-    int lo = 0, hi = ntab - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (table[mid].begin <= i) lo = mid; else hi = mid - 1;
+                                                           const TDesc* __restrict__ table, int ntab) {
+  __shared__ bf16_t tile[TF_T * TF_PITCH];
+  // descriptor owning this tile (uniform scalar binary search)
+  const int64_t b = blockIdx.x;
+  int lo = 0, hi = ntab - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (table[mid].begin <= b) lo = mid; else hi = mid - 1;
+  }
+  const TDesc d = table[lo];
+  int t = (int)(b - d.begin);
+  const int taps = d.Ru * d.Sv;
+  const int uv = t % taps; t /= taps;
+  const int kt = t % d.tk, ct = t / d.tk;
+  const int u = uv / d.Sv, v = uv - u * d.Sv;
+  const int rs = d.r0 + d.dr * u, ss = d.s0 + d.ds * v;
+  const int k0 = kt * TF_T, c0 = ct * TF_T;
+  const int tid = threadIdx.x, ch = tid & 7, row = tid >> 3;  // 8 chunks of 8 elements x 32 rows
+  const int64_t kstride = (int64_t)d.R * d.S * d.C;
+  const bf16_t* src = w + d.src + ((int64_t)rs * d.S + ss) * d.C;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = k0 + row + h * 32, c = c0 + ch * 8;
+    uint4 val = make_uint4(0, 0, 0, 0);
+    if (k < d.K && c < d.C) val = *reinterpret_cast<const uint4*>(src + k * kstride + c);
+    uint32_t* l = reinterpret_cast<uint32_t*>(tile + (row + h * 32) * TF_PITCH + ch * 8);
+    l[0] = val.x; l[1] = val.y; l[2] = val.z; l[3] = val.w;
+  }
+  __syncthreads();
+  bf16_t* dst = wt + d.dst + (int64_t)uv * d.K;
+  const int64_t cstride = (int64_t)taps * d.K;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int cl = row + h * 32, c = c0 + cl, k = k0 + ch * 8;
+    if (c < d.C && k < d.K) {
+      uint32_t o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t lo16 = tile[(ch * 8 + 2 * j) * TF_PITCH + cl];
+        const uint32_t hi16 = tile[(ch * 8 + 2 * j + 1) * TF_PITCH + cl];
+        o[j] = lo16 | (hi16 << 16);
+      }
+      *reinterpret_cast<uint4*>(dst + c * cstride + k) = make_uint4(o[0], o[1], o[2], o[3]);
     }
-    const TDesc d = table[lo];
-    int64_t e = i - d.begin;  // index into destination [C][Ru][Sv][K]
-    const int k = (int)(e % d.K); e /= d.K;
-    const int v = (int)(e % d.Sv); e /= d.Sv;
-    const int u = (int)(e % d.Ru);
-    const int c = (int)(e / d.Ru);
-    const int rs = d.r0 + d.dr * u, ssrc = d.s0 + d.ds * v;
-    wt[d.dst + i - d.begin] = w[d.src + (((int64_t)k * d.R + rs) * d.S + ssrc) * d.C + c];
   }
 }
 
@@ -108,9 +143,11 @@ DRN_API int drn_cast_bf16(const float* x, void* y, int64_t n, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// total = number of tiles (last begin + its count); every descriptor has K % 8 == C % 8 == 0.
 DRN_API int drn_weight_tflip(const void* w, void* wt, const void* table, int ntab, int64_t total, hipStream_t s) {
-  hipLaunchKernelGGL(drn::weight_tflip_kernel, dim3(drn::grid_for(total)), dim3(256), 0, s, (const bf16_t*)w,
-                     (bf16_t*)wt, (const drn::TDesc*)table, ntab, total);
+  if (ntab < 1 || total < 1 || total > 0x7fffffff) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(drn::weight_tflip_kernel, dim3((unsigned)total), dim3(256), 0, s, (const bf16_t*)w,
+                     (bf16_t*)wt, (const drn::TDesc*)table, ntab);
   return (int)hipGetLastError();
 }
 

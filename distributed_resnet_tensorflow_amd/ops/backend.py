@@ -49,7 +49,7 @@ def dgrad_geom(g: ConvGeom, R: int, S: int) -> ConvGeom:
 
 TDESC = np.dtype([("src", "<i8"), ("dst", "<i8"), ("K", "<i4"), ("R", "<i4"), ("S", "<i4"), ("C", "<i4"),
                   ("Ru", "<i4"), ("Sv", "<i4"), ("r0", "<i4"), ("s0", "<i4"), ("dr", "<i4"), ("ds", "<i4"),
-                  ("p0", "<i4"), ("p1", "<i4"), ("begin", "<i8")])  # mirror of sgd.hip `struct TDesc`
+                  ("tk", "<i4"), ("tc", "<i4"), ("begin", "<i8")])  # mirror of sgd.hip `struct TDesc`
 
 
 def tflip_desc(src, dst, K, R, S, C, Ru=None, Sv=None, r0=None, s0=None, dr=-1, ds=-1):
@@ -62,13 +62,18 @@ def tflip_desc(src, dst, K, R, S, C, Ru=None, Sv=None, r0=None, s0=None, dr=-1, 
 
 
 def tflip_table(descs):
-    """Pack descriptors (see tflip_desc) into the byte table of drn_weight_tflip."""
+    """Pack descriptors (see tflip_desc) into the byte table of drn_weight_tflip: the kernel is a
+    tiled transpose with one workgroup per (descriptor, tap, 64 k, 64 c) tile; `begin` is the
+    tile prefix sum and the returned total is the tile count (= the launch grid)."""
     arr = np.zeros(max(1, len(descs)), dtype=TDESC)
     begin = 0
     for i, d in enumerate(descs):
         src, dst, K, R, S, C, Ru, Sv, r0, s0, dr, ds = d
-        arr[i] = (src, dst, K, R, S, C, Ru, Sv, r0, s0, dr, ds, 0, 0, begin)
-        begin += C * Ru * Sv * K
+        if K % 8 or C % 8:
+            raise ValueError(f"weight_tflip needs K and C multiples of 8 (got K={K}, C={C})")
+        tk, tc = -(-K // 64), -(-C // 64)
+        arr[i] = (src, dst, K, R, S, C, Ru, Sv, r0, s0, dr, ds, tk, tc, begin)
+        begin += Ru * Sv * tk * tc
     return torch.from_numpy(arr.view(np.uint8).copy()), len(descs), begin
 
 

@@ -405,9 +405,14 @@ def test_sgd_and_tflip(hip, ref):
     for a, b in zip(res["hip"], res["ref"]):
         assert rel(a, b) < 4e-3
     # transpose-flip
-    descs = [tflip_desc(0, 0, 16, 3, 3, 8), tflip_desc(16 * 9 * 8, 16 * 9 * 8, 32, 1, 1, 16),
-             tflip_desc(0, 16 * 9 * 8 + 32 * 16, 16, 3, 3, 8, Ru=2, Sv=1, r0=2, s0=1, dr=-2, ds=-2)]
-    tot = 16 * 9 * 8 + 32 * 16 + 16 * 2 * 8
+    o1 = 16 * 9 * 8
+    o2 = o1 + 32 * 16
+    o3 = o2 + 16 * 2 * 8
+    descs = [tflip_desc(0, 0, 16, 3, 3, 8), tflip_desc(o1, o1, 32, 1, 1, 16),
+             tflip_desc(0, o2, 16, 3, 3, 8, Ru=2, Sv=1, r0=2, s0=1, dr=-2, ds=-2),
+             tflip_desc(o3, o3, 136, 3, 3, 200),  # partial 64-wide tiles on both axes
+             tflip_desc(o3, o3 + 136 * 9 * 200, 136, 3, 3, 200, Ru=1, Sv=2, r0=1, s0=2, dr=-2, ds=-2)]
+    tot = o3 + 136 * 9 * 200 + 136 * 2 * 200
     wflat = torch.randn(tot)
     table, nt, total = tflip_table(descs)
     out_ref = torch.zeros(tot)
@@ -415,7 +420,7 @@ def test_sgd_and_tflip(hip, ref):
     out_hip = torch.zeros(tot, dtype=torch.bfloat16, device="cuda")
     hip.weight_tflip(bf(wflat).cuda(), out_hip, table.cuda(), nt, total)
     torch.cuda.synchronize()
-    assert rel(out_hip, out_ref) < 1e-2
+    assert torch.equal(out_hip.float().cpu(), bf(out_ref).float())
 
 
 def test_cifar_augment(hip, ref):
