@@ -61,7 +61,13 @@ def main():
     if os.environ.get("DRN_BENCH_ONE_DEVICE") == "1":
         local = 0
     torch.cuda.set_device(local)
-    if world > 1:
+    # DRN_BENCH_DP=1: run the data-parallel engine (single-rank process group) even at N=1, to
+    # measure the DP step machinery on one GPU
+    force_dp = os.environ.get("DRN_BENCH_DP") == "1"
+    if force_dp and world == 1 and "MASTER_ADDR" not in os.environ:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("DRN_BENCH_PORT", "29533"),
+                          RANK="0", WORLD_SIZE="1")
+    if world > 1 or force_dp:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -70,14 +76,15 @@ def main():
     from distributed_resnet_tensorflow_amd.models.spec import build_spec
     from distributed_resnet_tensorflow_amd.ops.backend import HipBackend
     from distributed_resnet_tensorflow_amd.runtime.executor import Executor
-    from distributed_resnet_tensorflow_amd.runtime.graph import StepGraph
+    from distributed_resnet_tensorflow_amd.runtime.graph import SegmentedStepGraph, StepGraph
     from distributed_resnet_tensorflow_amd.parallel.engine import DataParallelEngine
 
     spec = build_spec(args.dataset, args.resnet_size, width=args.width)
     be = HipBackend("cuda")
     wd = 2e-4 if args.dataset == "cifar10" else 1e-4
     ex = Executor(spec, args.batch_size, be, "cuda", seed=1234, weight_decay=wd)
-    eng = DataParallelEngine(ex, bucket_mb=args.bucket_mb, allreduce=args.allreduce) if world > 1 else None
+    eng = DataParallelEngine(ex, bucket_mb=args.bucket_mb, allreduce=args.allreduce) if (world > 1 or force_dp) \
+        else None
     if eng is not None:
         eng.broadcast_parameters()
     # synthetic data of the benchmark shape: fixed device batch (no host input pipeline)
@@ -100,9 +107,16 @@ def main():
     # kernel autotuning pass (one plain forward + backward) before any collective is in flight,
     # so every rank times its candidate kernels on an otherwise idle GPU
     ex.autotune()
-    use_graph = args.graph if args.graph >= 0 else int(world == 1)
+    # one GPU: the whole step in one HIP graph. N GPUs: eager by default -- measured on one GPU
+    # with the single-rank RCCL engine, eager 11.90 ms vs per-segment graphs (--graph 1,
+    # runtime/graph.py SegmentedStepGraph, bucket all-reduces issued between graphs) 12.22 ms:
+    # the ~20 graph launches cost more than the host-side kernel launches they replace
+    use_graph = args.graph if args.graph >= 0 else int(eng is None)
     run = step
-    if use_graph:
+    if use_graph and eng is not None and eng.p2p is None:
+        sg = SegmentedStepGraph(ex, eng, 1.0 / world, warmup=1)
+        run = sg.replay
+    elif use_graph:
         sg = StepGraph(step, warmup=2)
         run = sg.replay
     for _ in range(args.warmup):

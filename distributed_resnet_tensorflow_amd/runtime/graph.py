@@ -4,7 +4,9 @@ CIFAR-size steps are ~500 kernel launches of a few microseconds each, so host la
 dominate. The executor issues every launch on the current stream with raw
 device pointers into pre-allocated buffers and reads the learning rate from device memory, so the
 complete forward + backward (+ all-reduce) + SGD sequence is captured once with
-``torch.cuda.CUDAGraph`` (= hipGraph on ROCm) and replayed per step.
+``torch.cuda.CUDAGraph`` (= hipGraph on ROCm) and replayed per step. Data-parallel steps whose
+collectives are host-issued RCCL calls use a chain of per-segment graphs instead
+(SegmentedStepGraph).
 """
 from __future__ import annotations
 
@@ -30,3 +32,74 @@ class StepGraph:
 
     def replay(self):
         self.graph.replay()
+
+
+class SegmentedStepGraph:
+    """Data-parallel step as a chain of HIP graphs with the gradient collectives between them.
+
+    RCCL collectives are issued from the host (`torch.distributed`), so instead of capturing
+    them the step is cut at the executor's gradient-ready points: graph i ends at the i-th
+    `grad_ready(lo)` report of the backward (graph 0 also holds the forward), the last graph is
+    the fused SGD update. Replay launches each graph and then hands its `lo` to the engine, which
+    fires every bucket that became complete on RCCL's stream -- the same overlap as the eager
+    path, at ~20 graph launches per step instead of ~450 kernel launches (eager ImageNet
+    ResNet-50 is host-bound).
+    All buffers are preallocated by the executor, so no capture allocates.
+    """
+
+    def __init__(self, ex, engine, grad_scale: float, warmup: int = 1):
+        if engine.p2p is not None or engine.mode != "sync":
+            raise ValueError("segmented graphs are for the synchronous RCCL/gloo engine")
+        self.ex, self.eng, self.grad_scale = ex, engine, grad_scale
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._eager()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self.segments = []   # (graph, lo reported after it); the last graph runs after finish()
+        self._g = None
+        with torch.cuda.stream(s):
+            self._open()
+            ex.forward(train=True)
+            ex.grad_ready = self._cut       # backward ends with grad_ready(0): the open graph
+            try:                            # then holds only the SGD update
+                ex.backward()
+            finally:
+                ex.grad_ready = None
+            ex.apply_gradients(grad_scale=grad_scale, grad=ex.P.grad)
+            self._close(None)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+
+    def _eager(self):
+        ex, eng = self.ex, self.eng
+        ex.forward(train=True)
+        eng.begin_step()
+        ex.backward()
+        g = eng.finish()
+        ex.apply_gradients(grad_scale=self.grad_scale, grad=g)
+
+    def _open(self):
+        self._g = torch.cuda.CUDAGraph()
+        self._g.capture_begin()
+
+    def _close(self, lo):
+        self._g.capture_end()
+        self.segments.append((self._g, lo))
+        self._g = None
+
+    def _cut(self, lo: int):
+        self._close(lo)
+        self._open()
+
+    def replay(self):
+        eng = self.eng
+        eng.begin_step()
+        eng.ex.grad_ready = None          # the recorded cut points stand in for the hook
+        for g, lo in self.segments[:-1]:
+            g.replay()
+            eng._on_ready(lo)
+        eng.finish()
+        self.segments[-1][0].replay()

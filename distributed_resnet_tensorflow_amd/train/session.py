@@ -9,6 +9,7 @@ overlapped with backward) + fused SGD].
 from __future__ import annotations
 
 import logging
+import os
 import time
 from typing import Callable, List, Optional
 
@@ -18,7 +19,7 @@ from ..ckpt.saver import Saver, latest_checkpoint
 from ..ops.backend import HipBackend, RefBackend
 from ..parallel.engine import DataParallelEngine
 from ..runtime.executor import Executor
-from ..runtime.graph import StepGraph
+from ..runtime.graph import SegmentedStepGraph, StepGraph
 from ..runtime.state import export_state, import_state
 from .hooks import Hook
 
@@ -52,7 +53,11 @@ class TrainingSession:
         self._restore()
         if self.device.type == "cuda":
             self.ex.autotune()  # fix kernel configurations before any collective / graph capture
-        self.use_graph = use_graph and self.device.type == "cuda" and not cluster.distributed
+        # one GPU: the whole step is one HIP graph. Data parallel: eager (measured faster than the
+        # chain of per-segment graphs, SegmentedStepGraph, which DRN_DP_GRAPH=1 selects)
+        self.use_graph = use_graph and self.device.type == "cuda" and (
+            not cluster.distributed or (os.environ.get("DRN_DP_GRAPH") == "1" and self.engine.p2p is None
+                                        and self.engine.mode == "sync"))
         self._graph: Optional[StepGraph] = None
         self._metrics_cache = None
         self.cur_lr = float("nan")
@@ -102,8 +107,11 @@ class TrainingSession:
         self.cur_lr = self.lr.lr_for_step()
         self.ex.set_lr(self.cur_lr)
         if self.use_graph and not self.ex.check_nan:  # the debug checks synchronize: no capture
-            if self._graph is None:
-                self._graph = StepGraph(self._step_body, warmup=1)  # warm-up = this real step
+            if self._graph is None:  # warm-up = this real step
+                if self.engine is not None:
+                    self._graph = SegmentedStepGraph(self.ex, self.engine, 1.0 / self.world, warmup=1)
+                else:
+                    self._graph = StepGraph(self._step_body, warmup=1)
             else:
                 self._graph.replay()
         else:

@@ -24,10 +24,10 @@ def _free_port():
     return p
 
 
-def _make(spec, N, shard, seed):
+def _make(spec, N, shard, seed, be=None):
     from distributed_resnet_tensorflow_amd.ops.backend import HipBackend
     from distributed_resnet_tensorflow_amd.runtime.executor import Executor
-    ex = Executor(spec, N, HipBackend("cuda"), "cuda", seed=seed)
+    ex = Executor(spec, N, be or HipBackend("cuda"), "cuda", seed=seed)
     g = torch.Generator().manual_seed(100 + shard)
     ex.images.zero_()
     ex.images[..., :3] = torch.randn(N, 32, 32, 3, generator=g).bfloat16().cuda()
@@ -93,10 +93,68 @@ def test_dp_engine_gpu_two_ranks_one_device(allreduce):
         p.join(timeout=60)
     for rank, err, same in res:
         assert isinstance(err, float), err
-        # bf16 kernels with fp32 atomics in BN statistics: the two computations of the same
-        # replica gradient agree to bf16 level, not bitwise
-        assert err < 2e-2, (rank, err)
+        # bf16 kernels with fp32 atomics in BN statistics, and each executor autotunes its own
+        # conv configs (different summation orders): the two computations of the same replica
+        # gradient agree to bf16 level through 8 layers at batch 8, not bitwise; a lost or doubled
+        # bucket shows up as an O(1) error
+        assert err < 5e-2, (rank, err)
         assert same
+
+
+def _seg_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2
+        from distributed_resnet_tensorflow_amd.parallel.engine import DataParallelEngine
+        from distributed_resnet_tensorflow_amd.runtime.graph import SegmentedStepGraph
+        from distributed_resnet_tensorflow_amd.ops.backend import HipBackend
+        spec, N = cifar_resnet_v2(8), 8
+        exs, engs = [], []
+        be = HipBackend("cuda")                 # one backend: identical tuned kernel configs
+        for _ in range(2):
+            ex = _make(spec, N, rank, seed=1 + rank, be=be)
+            ex.set_lr(0.1)
+            eng = DataParallelEngine(ex, bucket_mb=0.05)
+            eng.broadcast_parameters()
+            exs.append(ex)
+            engs.append(eng)
+        ea, eb = exs
+        for _ in range(3):                      # eager reference: 3 steps
+            ea.forward(True)
+            engs[0].begin_step()
+            ea.backward()
+            ea.apply_gradients(grad_scale=1.0 / world, grad=engs[0].finish())
+        sg = SegmentedStepGraph(eb, engs[1], 1.0 / world, warmup=1)   # 1 eager + 2 replays
+        sg.replay()
+        sg.replay()
+        torch.cuda.synchronize()
+        err = ((ea.P.master - eb.P.master).norm() / ea.P.master.norm()).item()
+        q.put((rank, err, len(sg.segments) > 3 and bool(torch.isfinite(eb.P.master).all())))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), False))
+
+
+def test_segmented_graph_dp_step_matches_eager():
+    """Per-segment HIP graphs with host-issued all-reduces between them (the N>1 bench / training
+    path) reproduce the eager data-parallel step."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_seg_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, err, ok in res:
+        assert isinstance(err, float), err
+        assert err < 5e-3, (rank, err)
+        assert ok
 
 
 def test_bench_multirank_code_path_one_device():
