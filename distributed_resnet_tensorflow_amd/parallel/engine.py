@@ -15,10 +15,11 @@ the executor reports, after every residual block's backward, the lowest flat off
 gradients are complete, and every bucket that is fully complete is all-reduced immediately
 (async op on RCCL's stream, ordered after the producing kernels) while earlier blocks are still
 back-propagating. `finish()` makes the compute stream wait for the last bucket before the
-fused SGD launch. The average's 1/N is folded into the SGD kernel (grad_scale). Bucket size
-default 25 MB: ResNet-50's 102 MB of fp32 gradients -> 5 buckets, each large enough to run
-RCCL at link bandwidth on the 7 point-to-point xGMI links of an 8-GPU node and small enough
-that only the last (smallest-layer) bucket is exposed after backward.
+fused SGD launch. The average's 1/N is folded into the SGD kernel (grad_scale). Bucket sizes
+grow from 2 MB at the start of the buffer (stem / stage 1, produced last) to the 25 MB cap:
+ResNet-50's 102 MB of fp32 gradients -> 3 large buckets that run RCCL at link bandwidth on the
+7 point-to-point xGMI links while the backward pass continues, and small final buckets, so only
+~2 MB of all-reduce is left exposed after the backward pass.
 
 Async PS training (--sync_replicas=False with --job_name set) maps to
 `mode="delayed"`: step t applies the averaged gradient of step t-1 while step t's all-reduce
@@ -34,14 +35,14 @@ import torch.distributed as dist
 
 class DataParallelEngine:
     def __init__(self, executor, bucket_mb: float = 25.0, mode: str = "sync", group=None,
-                 allreduce: str = "rccl", p2p_max_mb: float = 64.0):
+                 allreduce: str = "rccl", p2p_max_mb: float = 64.0, first_bucket_mb: float = 2.0):
         self.ex = executor
         self.P = executor.P
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.mode = mode
-        self.buckets = self._make_buckets(int(bucket_mb * (1 << 20) // 4))
+        self.buckets = self._make_buckets(int(bucket_mb * (1 << 20) // 4), int(first_bucket_mb * (1 << 20) // 4))
         # --allreduce: rccl | p2p (one-shot HIP IPC kernel, parallel/p2p.py) | auto (p2p when the
         # whole gradient is small -- latency-bound CIFAR buckets -- and the job is one GPU node)
         self.p2p = None
@@ -62,19 +63,22 @@ class DataParallelEngine:
             self.ready_grad = torch.zeros_like(self.P.grad)
 
     # -- bucket layout ---------------------------------------------------------------------------
-    def _make_buckets(self, cap_elems: int):
-        """Contiguous [lo, hi) slices from the END of the flat buffer, cut at slot boundaries."""
+    def _make_buckets(self, cap_elems: int, first_elems: int = 0):
+        """Contiguous [lo, hi) slices cut at slot boundaries, returned in the order they become
+        ready (end of the flat buffer first). Sizes grow geometrically from the START of the
+        buffer (the stem / first stage, whose gradients are produced last): first_elems, 2x, 4x,
+        ... capped at cap_elems, so the bucket left exposed after the backward pass is small
+        while the early (large-layer) buckets stay large enough for link-bandwidth RCCL."""
         bounds = [s.offset for s in self.P.slots] + [self.P.total]
-        buckets = []
-        hi = self.P.total
-        for i in range(len(bounds) - 2, -1, -1):
-            lo = bounds[i]
-            if hi - lo >= cap_elems and lo != hi:
-                buckets.append((lo, hi))
-                hi = lo
-        if hi > 0:
-            buckets.append((0, hi))
-        return buckets  # ordered from the end of the buffer (first ready) to the start
+        first_elems = min(first_elems or cap_elems, cap_elems)
+        buckets, lo, want = [], 0, first_elems
+        for b in bounds[1:]:
+            if b - lo >= want:
+                buckets.append((lo, b))
+                lo, want = b, min(2 * want, cap_elems)
+        if lo < self.P.total:
+            buckets.append((lo, self.P.total))
+        return buckets[::-1]
 
     # -- hooks --------------------------------------------------------------------------------------
     def begin_step(self):

@@ -76,12 +76,12 @@ def _worker(rank, world, port, mode, q):
         q.put((rank, repr(e) + traceback.format_exc(), False))
 
 
-@pytest.mark.parametrize("mode", ["sync", "delayed"])
-def test_allreduce_dp_equals_mean_of_replica_gradients(mode):
+@pytest.mark.parametrize("mode,world", [("sync", 2), ("delayed", 2), ("sync", 4)])
+def test_allreduce_dp_equals_mean_of_replica_gradients(mode, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=300) for _ in ps]
@@ -91,3 +91,25 @@ def test_allreduce_dp_equals_mean_of_replica_gradients(mode):
         assert isinstance(err, float), err
         assert err < 1e-5, (rank, err)
         assert same
+
+
+def test_bucket_layout_grows_from_the_buffer_start():
+    """Buckets tile the flat gradient buffer exactly, at slot (tensor) boundaries, in readiness
+    order (end of the buffer first), and grow geometrically from the start so that the bucket
+    exposed after the backward pass is small (ImageNet ResNet-50: 25 MB cap, 2 MB first)."""
+    from distributed_resnet_tensorflow_amd.models.spec import build_spec
+    from distributed_resnet_tensorflow_amd.parallel.engine import DataParallelEngine
+    from distributed_resnet_tensorflow_amd.runtime.params import ParamStore
+    P = ParamStore(build_spec("imagenet", 50), "cpu", False)
+    eng = DataParallelEngine.__new__(DataParallelEngine)
+    eng.P = P
+    mb = (1 << 20) // 4
+    b = eng._make_buckets(25 * mb, 2 * mb)
+    assert b[0][1] == P.total and b[-1][0] == 0
+    assert all(b[i][0] == b[i + 1][1] for i in range(len(b) - 1))
+    offs = {s.offset for s in P.slots}
+    assert all(lo in offs for lo, _ in b)
+    largest = max(s.numel for s in P.slots)
+    assert (b[-1][1] - b[-1][0]) <= 2 * mb + largest
+    assert (b[-1][1] - b[-1][0]) < 4 * mb        # ~2 MB exposed, not a 25 MB bucket
+    assert max(hi - lo for lo, hi in b) < 30 * mb
