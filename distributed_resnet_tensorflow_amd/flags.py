@@ -223,7 +223,9 @@ def define_reference_flags(flag_values: FlagValues = FLAGS, **defaults) -> FlagV
     S("profile_steps", "", "a:b -> roctx-mark and torch-profile steps a..b.", fv)
     S("allreduce", "rccl", "Gradient all-reduce: rccl (RCCL ring/tree over xGMI; gloo on CPU), p2p (one-shot "
       "HIP-IPC peer kernel, one node), auto (p2p when the gradient is <= 64 MB).", fv)
-    Fl("bucket_mb", 25.0, "Gradient all-reduce bucket size (MB of fp32).", fv)
+    Fl("bucket_mb", 25.0, "Gradient all-reduce bucket size cap (MB of fp32).", fv)
+    I("collective_timeout_secs", 600, "Process-group timeout and collective-watchdog limit: a rank whose "
+      "gradient exchange stalls this long exits (the launcher restarts the job from its checkpoint).", fv)
     I("fault_inject_step", -1, "Kill this process at the given global step (fault-injection tests).", fv)
     I("fault_inject_rank", 0, "Rank that --fault_inject_step applies to.", fv)
     B("hip_graph", True, "Capture the single-GPU training step in a HIP graph.", fv)

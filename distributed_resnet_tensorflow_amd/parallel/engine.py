@@ -27,15 +27,19 @@ runs behind step t+1's compute (bounded staleness 1, no PS).
 """
 from __future__ import annotations
 
+import time
 from typing import List, Optional
 
 import torch
 import torch.distributed as dist
 
+from .watchdog import CollectiveWatchdog
+
 
 class DataParallelEngine:
     def __init__(self, executor, bucket_mb: float = 25.0, mode: str = "sync", group=None,
-                 allreduce: str = "rccl", p2p_max_mb: float = 64.0, first_bucket_mb: float = 2.0):
+                 allreduce: str = "rccl", p2p_max_mb: float = 64.0, first_bucket_mb: float = 2.0,
+                 timeout_s: float = 0.0):
         self.ex = executor
         self.P = executor.P
         self.group = group
@@ -61,6 +65,13 @@ class DataParallelEngine:
         if mode == "delayed":
             self.comm_grad = torch.zeros_like(self.P.grad)
             self.ready_grad = torch.zeros_like(self.P.grad)
+        # observability: per-step backward time, all-reduce time left exposed after
+        # the backward pass, and the overlap fraction; device events on GPU, host clock on CPU
+        self.cuda = self.P.grad.is_cuda
+        self._ev = None
+        self._host_t = None
+        self._step_no = 0
+        self.watchdog = CollectiveWatchdog(timeout_s, rank=self.rank) if timeout_s > 0 else None
 
     # -- bucket layout ---------------------------------------------------------------------------
     def _make_buckets(self, cap_elems: int, first_elems: int = 0):
@@ -85,6 +96,16 @@ class DataParallelEngine:
         self.works = []
         self.launched = [False] * len(self.buckets)
         self.frontier = self.P.total
+        self._step_no += 1
+        if self.watchdog is not None:
+            self.watchdog.arm(self._step_no)
+        if self.cuda and torch.cuda.is_current_stream_capturing():
+            self._ev = self._host_t = None     # a whole-step graph capture: no timing events
+        elif self.cuda:
+            self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            self._ev[0].record()
+        else:
+            self._host_t = [time.perf_counter(), None, None]
         if self.p2p is not None:
             self.p2p.begin_step()
         if self.mode == "sync":
@@ -108,24 +129,40 @@ class DataParallelEngine:
             if not self.launched[i] and lo >= self.frontier:
                 self._launch(i)
 
+    def _mark(self, k: int):
+        if self._ev is not None:
+            self._ev[k].record()
+        elif self._host_t is not None:
+            self._host_t[k] = time.perf_counter()
+
+    def _done(self):
+        self._mark(2)
+        if self.watchdog is not None:
+            self.watchdog.done(self._ev[2] if self._ev is not None else None)
+
     def finish(self) -> torch.Tensor:
         """Complete the step's gradient exchange; returns the gradient buffer SGD must use."""
         if self.mode == "sync":
             for i in range(len(self.buckets)):
                 if not self.launched[i]:
                     self._launch(i)
+            self._mark(1)                      # backward done (all buckets issued)
             for w in self.works:
                 w.wait()
-            self.works = []
+            self._done_works, self.works = self.works, []
             self.ex.grad_ready = None
             if self.p2p is not None:
                 self.p2p.end_step()
+                self._done()
                 return self.p2p.out
+            self._done()
             return self.P.grad
         # delayed (async-PS analog): finish last step's exchange, start this step's
+        self._mark(1)
         for w in self.works:
             w.wait()
-        self.works = []
+        self._done_works, self.works = self.works, []
+        self._done()
         had = self._delayed_pending
         if had:
             self.ready_grad.copy_(self.comm_grad)
@@ -136,6 +173,35 @@ class DataParallelEngine:
             self._launch(i, self.comm_grad)
         self._delayed_pending = True
         return self.ready_grad
+
+    def stats(self) -> dict:
+        """Timing of the last completed step (synchronizes on its events)."""
+        out = {"allreduce_buckets": len(self.buckets)}
+        if self._ev is not None:
+            self._ev[2].synchronize()
+            bwd = self._ev[0].elapsed_time(self._ev[1])
+            exposed = self._ev[1].elapsed_time(self._ev[2])
+        elif self._host_t is not None and self._host_t[2] is not None:
+            bwd = (self._host_t[1] - self._host_t[0]) * 1e3
+            exposed = (self._host_t[2] - self._host_t[1]) * 1e3
+        else:
+            return out
+        out["backward_ms"] = bwd
+        out["comm_exposed_ms"] = max(exposed, 0.0)
+        works = getattr(self, "_done_works", [])
+        d = [_work_ms(w) for w in works]
+        if d and all(x is not None for x in d):
+            total = float(sum(d))      # RCCL kernel time (TORCH_NCCL_ENABLE_TIMING=1)
+            out["comm_ms"] = total
+            out["overlap_fraction"] = max(0.0, 1.0 - out["comm_exposed_ms"] / total) if total > 0 else 1.0
+        return out
+
+    def close(self):
+        if self.watchdog is not None:
+            self.watchdog.close()
+            self.watchdog = None
+        if self.p2p is not None:
+            self.p2p.close()
 
     # -- state sync -----------------------------------------------------------------------------------
     def broadcast_parameters(self, src: int = 0):
@@ -153,3 +219,13 @@ class DataParallelEngine:
         per replica and checkpoints the chief's copy, so this is off by default)."""
         dist.all_reduce(self.P.bn_state, op=dist.ReduceOp.SUM, group=self.group)
         self.P.bn_state.div_(self.world)
+
+
+def _work_ms(w) -> Optional[float]:
+    """Device time of a finished collective when the process group records it (RCCL with
+    TORCH_NCCL_ENABLE_TIMING=1); None otherwise."""
+    try:
+        d = w._get_duration()
+        return float(d) if d is not None and d >= 0 else None
+    except Exception:
+        return None

@@ -44,7 +44,7 @@ def evaluate(FLAGS, eval_batch_size: int = 100, max_evals: int = -1):
     FLAGS.job_name = None
     cluster = cl.resolve(FLAGS, env={})
     spec = model_spec_from_flags(FLAGS)
-    be = make_backend(cluster.device)
+    be = make_backend(cluster.device, getattr(FLAGS, "precision", "bf16"))
     ex = Executor(spec, eval_batch_size, be, cluster.device, weight_decay=WEIGHT_DECAY.get(FLAGS.dataset, 1e-4))
     writer = EventFileWriter(FLAGS.eval_dir) if FLAGS.eval_dir else None
     best_path = os.path.join(FLAGS.eval_dir, "best_precision.json") if FLAGS.eval_dir else None

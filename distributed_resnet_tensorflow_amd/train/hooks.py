@@ -41,9 +41,11 @@ class Hook:
 
 
 class LoggingHook(Hook):
-    def __init__(self, every_n: int, batch_per_step: int, metrics_path: Optional[str] = None, with_lr: bool = True):
+    def __init__(self, every_n: int, batch_per_step: int, metrics_path: Optional[str] = None, with_lr: bool = True,
+                 world: int = 1):
         self.n = max(1, every_n)
         self.bps = batch_per_step
+        self.world = max(1, world)
         self.metrics_path = metrics_path
         self.with_lr = with_lr
         self._t = None
@@ -61,11 +63,15 @@ class LoggingHook(Hook):
         steps = step - self._s
         m["steps_per_sec"] = steps / dt
         m["images_per_sec"] = steps * self.bps / dt
+        m["images_per_sec_per_gpu"] = m["images_per_sec"] / self.world
         self._t, self._s = now, step
         parts = [f"step = {step}", f"loss = {m['cost']:.5f}", f"precision = {m['precision']:.5f}"]
         if self.with_lr:
             parts.append(f"lr = {m['learning_rate']:.5g}")
         parts.append(f"({m['steps_per_sec']:.2f} steps/sec, {m['images_per_sec']:.1f} images/sec)")
+        if "comm_exposed_ms" in m:
+            parts.append(f"[allreduce exposed {m['comm_exposed_ms']:.2f} ms"
+                         + (f", overlap {m['overlap_fraction']:.0%}" if "overlap_fraction" in m else "") + "]")
         log.info(", ".join(parts))
         if self.metrics_path:
             with open(self.metrics_path, "a") as f:

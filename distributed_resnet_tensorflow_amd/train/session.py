@@ -26,8 +26,18 @@ from .hooks import Hook
 log = logging.getLogger("drn")
 
 
-def make_backend(device: str):
+def make_backend(device: str, precision: str = "bf16"):
+    """--precision: bf16 = the gfx950 HIP kernel library (bf16 activations / weights, fp32
+    accumulation, fp32 master weights, momentum and BN statistics); fp32 = the fp32 PyTorch
+    reference backend on the same device (a numerics-debugging path, not a performance one).
+    CPU runs always use the fp32 reference backend."""
+    if precision not in ("bf16", "fp32"):
+        raise ValueError(f"--precision must be bf16 or fp32, got {precision!r}")
     if str(device).startswith("cuda"):
+        if precision == "fp32":
+            log.warning("--precision=fp32: fp32 PyTorch reference ops on %s (debug path; the HIP kernels are bf16)",
+                        device)
+            return RefBackend(device)
         return HipBackend(device)
     return RefBackend("cpu")
 
@@ -35,27 +45,28 @@ def make_backend(device: str):
 class TrainingSession:
     def __init__(self, spec, batch: int, cluster, *, weight_decay: float, lr_schedule, checkpoint_dir: str = "",
                  max_to_keep: int = 5, seed: int = 0, use_graph: bool = True, sync_mode: str = "sync",
-                 bucket_mb: float = 25.0, meta: Optional[dict] = None, allreduce: str = "rccl"):
+                 bucket_mb: float = 25.0, meta: Optional[dict] = None, allreduce: str = "rccl",
+                 collective_timeout_s: float = 0.0, precision: str = "bf16"):
         self.cluster = cluster
         self.spec = spec
         self.device = torch.device(cluster.device)
-        self.be = make_backend(cluster.device)
+        self.be = make_backend(cluster.device, precision)
         self.ex = Executor(spec, batch, self.be, self.device, seed=seed, weight_decay=weight_decay)
         self.lr = lr_schedule
         self.meta = meta or {}
-        self.engine = DataParallelEngine(self.ex, bucket_mb=bucket_mb, mode=sync_mode,
-                                         allreduce=allreduce) if cluster.distributed else None
+        self.engine = DataParallelEngine(self.ex, bucket_mb=bucket_mb, mode=sync_mode, allreduce=allreduce,
+                                         timeout_s=collective_timeout_s) if cluster.distributed else None
         self.world = cluster.world
         self.ckpt_dir = checkpoint_dir
         self.saver = Saver(checkpoint_dir, max_to_keep) if (checkpoint_dir and cluster.is_chief) else None
         self.data_state = {}
         self.restored_from = None
         self._restore()
-        if self.device.type == "cuda":
+        if self.device.type == "cuda" and self.be.name == "hip":
             self.ex.autotune()  # fix kernel configurations before any collective / graph capture
         # one GPU: the whole step is one HIP graph. Data parallel: eager (measured faster than the
         # chain of per-segment graphs, SegmentedStepGraph, which DRN_DP_GRAPH=1 selects)
-        self.use_graph = use_graph and self.device.type == "cuda" and (
+        self.use_graph = use_graph and self.device.type == "cuda" and self.be.name == "hip" and (
             not cluster.distributed or (os.environ.get("DRN_DP_GRAPH") == "1" and self.engine.p2p is None
                                         and self.engine.mode == "sync"))
         self._graph: Optional[StepGraph] = None
@@ -121,9 +132,20 @@ class TrainingSession:
         self._metrics_cache = None
 
     def metrics(self) -> dict:
+        """Loss / precision / lr of the last step, plus the gradient exchange's
+        timing (backward_ms, comm_exposed_ms, comm_ms + overlap_fraction when the process group
+        records collective durations) and HBM usage."""
         if self._metrics_cache is None:
             m = self.ex.metrics()
             m["learning_rate"] = self.cur_lr
+            if self.engine is not None:
+                m.update(self.engine.stats())
+                if self.engine.p2p is not None:
+                    self.engine.p2p.check()
+            if self.device.type == "cuda":
+                free, total = torch.cuda.mem_get_info(self.device)
+                m["hbm_used_gb"] = (total - free) / 1e9
+                m["hbm_peak_alloc_gb"] = torch.cuda.max_memory_allocated(self.device) / 1e9
             self._metrics_cache = m
         return dict(self._metrics_cache)
 
@@ -148,3 +170,5 @@ class TrainingSession:
                 h.end(self)
             if self.saver is not None:
                 self.saver.wait()
+            if self.engine is not None:
+                self.engine.close()

@@ -81,7 +81,7 @@ def train(FLAGS, cluster=None):
     if FLAGS.model == "lrnet":
         from ..models.lrnet import train_lrnet
         return train_lrnet(FLAGS, cluster)
-    cl.init_process_group(cluster)
+    cl.init_process_group(cluster, timeout_s=FLAGS.collective_timeout_secs)
     torch.manual_seed(FLAGS.seed)
     spec = model_spec_from_flags(FLAGS)
     if cluster.is_chief:
@@ -97,12 +97,13 @@ def train(FLAGS, cluster=None):
     sess = TrainingSession(spec, FLAGS.batch_size, cluster, weight_decay=wd, lr_schedule=lr_mod.for_dataset(FLAGS.dataset),
                            checkpoint_dir=FLAGS.log_root, max_to_keep=FLAGS.max_to_keep, seed=FLAGS.seed,
                            use_graph=FLAGS.hip_graph, sync_mode=sync_mode, bucket_mb=FLAGS.bucket_mb,
-                           meta=_meta(FLAGS, spec), allreduce=FLAGS.allreduce)
+                           meta=_meta(FLAGS, spec), allreduce=FLAGS.allreduce,
+                           collective_timeout_s=FLAGS.collective_timeout_secs, precision=FLAGS.precision)
     feeder = make_feeder(FLAGS, sess.ex, cluster, True, sess.data_state)
     is_imagenet = FLAGS.dataset == "imagenet"
     hooks = [LoggingHook(FLAGS.log_every_n_steps, FLAGS.batch_size * cluster.world,
                          metrics_path=os.path.join(FLAGS.log_root, "metrics.jsonl") if (FLAGS.log_root and cluster.is_chief) else None,
-                         with_lr=not is_imagenet),
+                         with_lr=not is_imagenet, world=cluster.world),
              StopAtStepHook(FLAGS.train_steps)]
     if FLAGS.fault_inject_step >= 0:
         hooks.append(FaultInjectHook(FLAGS.fault_inject_step, FLAGS.fault_inject_rank, cluster.rank))

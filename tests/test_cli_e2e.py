@@ -72,6 +72,12 @@ def test_two_worker_fake_cluster(cifar_dir, tmp_path):
     outs = [p.communicate(timeout=600)[0] for p in ps]
     assert all(p.returncode == 0 for p in ps), outs
     assert "global step 6" in outs[0] and os.path.exists(os.path.join(ck, "model.ckpt-6.index"))
+    # SURVEY §5.5 metrics: throughput per node and per GPU, gradient-exchange timing
+    import json
+    recs = [json.loads(l) for l in open(os.path.join(ck, "metrics.jsonl"))]
+    assert recs and all(k in recs[-1] for k in ("images_per_sec", "images_per_sec_per_gpu", "steps_per_sec",
+                                                "backward_ms", "comm_exposed_ms"))
+    assert abs(recs[-1]["images_per_sec"] - 2 * recs[-1]["images_per_sec_per_gpu"]) < 1e-6 * recs[-1]["images_per_sec"]
 
 
 def test_launcher_fault_injection_and_restart(cifar_dir, tmp_path):

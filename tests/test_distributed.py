@@ -50,6 +50,8 @@ def _worker(rank, world, port, mode, q):
         eng.begin_step()
         ex.backward()
         g = eng.finish()
+        st = eng.stats()
+        assert st["comm_exposed_ms"] >= 0 and st["backward_ms"] > 0, st
         if mode == "sync":
             err = ((g / world - exp).norm() / exp.norm()).item()
             w_before = ex.P.master.clone()
@@ -113,3 +115,40 @@ def test_bucket_layout_grows_from_the_buffer_start():
     assert (b[-1][1] - b[-1][0]) <= 2 * mb + largest
     assert (b[-1][1] - b[-1][0]) < 4 * mb        # ~2 MB exposed, not a 25 MB bucket
     assert max(hi - lo for lo, hi in b) < 30 * mb
+
+
+def test_collective_watchdog_fires_on_stalled_exchange():
+    import time
+    from distributed_resnet_tensorflow_amd.parallel.watchdog import CollectiveWatchdog
+
+    class _Ev:
+        def __init__(self, ok):
+            self.ok = ok
+
+        def query(self):
+            return self.ok
+
+    msgs = []
+    # 1) host blocked inside the exchange (a gloo collective waiting for a dead peer)
+    wd = CollectiveWatchdog(0.2, on_timeout=msgs.append, poll_s=0.05)
+    wd.arm(7)
+    time.sleep(0.6)
+    assert wd.fired and "step 7" in msgs[-1] and "host" in msgs[-1]
+    wd.close()
+    # 2) queued on the device but never completing (an RCCL kernel stuck on a dead peer)
+    wd = CollectiveWatchdog(0.2, on_timeout=msgs.append, poll_s=0.05)
+    wd.arm(8)
+    wd.done(_Ev(False))
+    time.sleep(0.6)
+    assert wd.fired and "step 8" in msgs[-1] and "device" in msgs[-1]
+    wd.close()
+    # 3) healthy steps never fire
+    n = len(msgs)
+    wd = CollectiveWatchdog(0.2, on_timeout=msgs.append, poll_s=0.05)
+    for step in range(5):
+        wd.arm(step)
+        wd.done(_Ev(True))
+        time.sleep(0.1)
+    time.sleep(0.4)
+    assert not wd.fired and len(msgs) == n
+    wd.close()

@@ -162,3 +162,26 @@ def test_deterministic_mode_is_bitwise_reproducible(monkeypatch):
         outs.append((ex.P.master.clone(), ex.P.momentum.clone(), ex.P.bn_state.clone()))
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
+
+
+def test_precision_fp32_reference_backend_on_gpu():
+    """--precision=fp32: the executor runs the fp32 PyTorch reference backend on the GPU device
+    (debug path) and its step agrees with the bf16 HIP step to bf16 tolerance."""
+    from distributed_resnet_tensorflow_amd.train.session import make_backend
+    spec, N = cifar_resnet_v2(8), 8
+    out = {}
+    for prec in ("fp32", "bf16"):
+        be = make_backend("cuda", prec)
+        assert be.name == ("ref" if prec == "fp32" else "hip")
+        ex = Executor(spec, N, be, "cuda", seed=3)
+        g = torch.Generator().manual_seed(5)
+        ex.images.zero_()
+        ex.images[..., :3] = torch.randn(N, 32, 32, 3, generator=g).to(ex.images.dtype).cuda()
+        ex.labels.copy_(torch.randint(0, 10, (N,), generator=g, dtype=torch.int32))
+        ex.forward(True)
+        ex.backward()
+        torch.cuda.synchronize()
+        out[prec] = (ex.metrics()["cross_entropy"], ex.P.grad.clone())
+    assert abs(out["fp32"][0] - out["bf16"][0]) < 2e-2 * max(1.0, abs(out["fp32"][0]))
+    ga, gb = out["fp32"][1], out["bf16"][1]
+    assert ((ga - gb).norm() / ga.norm()).item() < 5e-2

@@ -37,3 +37,12 @@ def test_union_flags_present_everywhere():
 def test_unknown_flag_errors():
     with pytest.raises(flags.FlagsError):
         _fv()(["p", "--definitely_not_a_flag=1"])
+
+
+def test_precision_flag_validation():
+    import pytest as _pt
+    from distributed_resnet_tensorflow_amd.train.session import make_backend
+    assert make_backend("cpu", "fp32").name == "ref"
+    assert make_backend("cpu", "bf16").name == "ref"      # CPU: always the fp32 reference backend
+    with _pt.raises(ValueError):
+        make_backend("cpu", "fp16")
