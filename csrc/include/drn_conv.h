@@ -48,6 +48,27 @@ struct DrnConvFwdArgs {
   const float* bn_shift;
   const float* bn_mean;
   const float* bn_invstd;
+  // Optional fused BatchNorm finalize (needs stats): the workgroups of each BC-wide channel
+  // column count themselves in fin_cnt[c0 / BC]; the last to arrive sums the stats replicas of
+  // its channels and writes the BN parameters -- forward: fin_scale/shift/mean/invstd and the
+  // moving averages; with bn_x set: fin_dgamma = sum g*xhat, fin_dbeta = sum g and
+  // fin_coef[3][K] = (gamma*invstd, mean g, mean g*xhat) -- then re-arms its counter. Replaces
+  // the separate finalize launch; with a multi-launch output (phase-decomposed data gradient)
+  // only the last launch carries it.
+  unsigned* fin_cnt;
+  float fin_count, fin_eps, fin_momentum;
+  int32_t fin_pad_;
+  const float* fin_gamma;
+  const float* fin_beta;
+  float* fin_run_mean;
+  float* fin_run_var;
+  float* fin_scale;
+  float* fin_shift;
+  float* fin_mean;
+  float* fin_invstd;
+  float* fin_dgamma;
+  float* fin_dbeta;
+  float* fin_coef;
 };
 
 // dW[K][R][S][C] (+)= sum_{n,p,q} dy[n,p,q,k] * x[n, p*st-pad+r, q*st-pad+s, c]

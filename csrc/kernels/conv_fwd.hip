@@ -77,6 +77,65 @@ __device__ __forceinline__ void epi_prefetch(const DrnConvFwdArgs& a, int m0, in
   }
 }
 
+// Last-arriving workgroup of a channel column finalizes that column's BatchNorm (see
+// DrnConvFwdArgs::fin_cnt). The statistics atomics and the arrival counter are agent-scope
+// atomics, performed past the per-XCD L2s; every thread waits for its own atomics to complete
+// (vmcnt(0)) before the barrier and thread 0's counter increment, and the last workgroup reads
+// the replicas with agent-scope loads. No agent-scope fence: on gfx950 that writes back the
+// whole L2 (buffer_wbl2), which, issued by every workgroup, costs several times the conv.
+// The flag word lives in the (by now free) epilogue staging LDS: a static __shared__ variable
+// would add an LDS allocation granule to every instantiation and cost the 32 KB configurations
+// their fifth workgroup per CU.
+template <int BP, int BC, int NT>
+__device__ __forceinline__ void bn_fin_column(const DrnConvFwdArgs& a, int c0, int M, int* s_last) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // also: every thread is done with the staging LDS
+  const int col = c0 / BC;
+  if (threadIdx.x == 0) {
+    const unsigned tiles = (unsigned)((M + BP - 1) / BP);
+    *s_last = __hip_atomic_fetch_add(a.fin_cnt + col, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u == tiles;
+  }
+  __syncthreads();
+  if (!*s_last) return;
+  const int rep = a.stats_rep > 1 ? a.stats_rep : 1;
+  const int K = a.K;
+  for (int cl = threadIdx.x; cl < BC; cl += NT) {
+    const int c = c0 + cl;
+    if (c >= K) break;
+    float s = 0.f, q = 0.f;
+    for (int r = 0; r < rep; ++r) {
+      s += __hip_atomic_load(a.stats + (size_t)(2 * r) * K + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      q += __hip_atomic_load(a.stats + (size_t)(2 * r + 1) * K + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (a.bn_x != nullptr) {
+      a.fin_dbeta[c] = s;
+      a.fin_dgamma[c] = q;
+      a.fin_coef[c] = a.fin_gamma[c] * a.bn_invstd[c];
+      a.fin_coef[K + c] = s / a.fin_count;
+      a.fin_coef[2 * K + c] = q / a.fin_count;
+    } else {
+      const double mean = (double)s / a.fin_count;
+      double var = (double)q / a.fin_count - mean * mean;
+      if (var < 0.0) var = 0.0;
+      const float invstd = (float)(1.0 / sqrt(var + (double)a.fin_eps));
+      const float sc = a.fin_gamma[c] * invstd;
+      a.fin_scale[c] = sc;
+      a.fin_shift[c] = a.fin_beta[c] - (float)mean * sc;
+      a.fin_mean[c] = (float)mean;
+      a.fin_invstd[c] = invstd;
+      if (a.fin_run_mean != nullptr) {  // TF fused BN: the unbiased batch variance feeds the moving variance
+        const float n = a.fin_count;
+        const float unbiased = n > 1.f ? (float)(var * n / (n - 1.0)) : (float)var;
+        const float mo = a.fin_momentum;
+        a.fin_run_mean[c] = mo * a.fin_run_mean[c] + (1.f - mo) * (float)mean;
+        a.fin_run_var[c] = mo * a.fin_run_var[c] + (1.f - mo) * unbiased;
+      }
+    }
+  }
+  if (threadIdx.x == 0)  // re-arm: the next launch is stream-ordered after this one
+    __hip_atomic_store(a.fin_cnt + col, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // The fp32 accumulator tile is staged through LDS ([BP][BC] fp32, 16-byte chunks XOR-swizzled
 // by row: conflict-free 8-lane ds_write_b128 groups and 16-lane ds_read_b128 groups), then
 // written as whole 2*BC-byte pixel rows per wave instruction (fully coalesced). Optional
@@ -182,6 +241,7 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
       const int rep = a.stats_rep > 1 ? a.stats_rep : 1;
       if (c0 + cl < a.K) atomicAdd(a.stats + ((size_t)(blockIdx.x % rep) * 2 + which) * a.K + c0 + cl, s);
     }
+    if (a.fin_cnt != nullptr) bn_fin_column<BP, BC, NT>(a, c0, M, reinterpret_cast<int*>(smem));
   }
 }
 
@@ -711,6 +771,7 @@ DRN_API int drn_conv_glds_ok(const DrnConvFwdArgs* a) {
 // Dispatch on a->cfg; zero = >= 16 bytes of device zeros (the LDS-DMA loader's padding source).
 DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
   if ((a->C % 8) != 0 || (a->K % 8) != 0) return (int)hipErrorInvalidValue;
+  if (a->fin_cnt != nullptr && (a->stats == nullptr || a->K > 64 * 64)) return (int)hipErrorInvalidValue;
   if (drn_conv_glds_ok(a) && zero != nullptr && a->cfg != 100)
     return drn::launch_glds_cfg(a->cfg >= 0 ? a->cfg : drn::glds_default_cfg(a), a, zero, s);
   return drn_conv_fwd(a, s);
@@ -722,6 +783,7 @@ DRN_API int drn_conv_glds_default_cfg(const DrnConvFwdArgs* a) { return drn::gld
 
 DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s) {
   if ((a->C % 8) != 0 || (a->K % 8) != 0) return (int)hipErrorInvalidValue;
+  if (a->fin_cnt != nullptr && (a->stats == nullptr || a->K > 64 * 64)) return (int)hipErrorInvalidValue;
   if (a->dil != 1 && a->dil != 2) return (int)hipErrorInvalidValue;
   const bool pro = a->in_scale != nullptr;
   const bool dil2 = a->dil == 2;

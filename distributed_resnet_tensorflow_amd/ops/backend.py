@@ -20,6 +20,7 @@ from __future__ import annotations
 import ctypes
 import os
 from dataclasses import dataclass
+from typing import Optional
 
 import numpy as np
 import torch
@@ -82,6 +83,29 @@ def _aligned16(*ts):
     for t in ts:
         if t is not None and t.data_ptr() % 16:
             raise ValueError("per-channel BN buffers must be 16-byte aligned")
+
+
+@dataclass
+class BnFin:
+    """BatchNorm finalize fused into the convolution producing its statistics (the last-arriving
+    workgroup of each channel column; DrnConvFwdArgs.fin_cnt). Forward (no bn_bwd): scale/shift/
+    mean/invstd + moving averages from the sums; backward (with bn_bwd): dgamma, dbeta and the
+    apply coefficients coef[3][C]."""
+    counters: torch.Tensor            # int32, >= C/64 zeroed words (re-armed by the kernel)
+    count: float                      # rows N*H*W of the normalised tensor
+    gamma: torch.Tensor
+    beta: Optional[torch.Tensor] = None
+    run_mean: Optional[torch.Tensor] = None
+    run_var: Optional[torch.Tensor] = None
+    scale: Optional[torch.Tensor] = None
+    shift: Optional[torch.Tensor] = None
+    mean: Optional[torch.Tensor] = None
+    invstd: Optional[torch.Tensor] = None
+    dgamma: Optional[torch.Tensor] = None
+    dbeta: Optional[torch.Tensor] = None
+    coef: Optional[torch.Tensor] = None
+    momentum: float = 0.997
+    eps: float = 1e-5
 
 
 @dataclass(frozen=True)
@@ -150,7 +174,7 @@ class HipBackend(_Common):
 
     # -- conv ---------------------------------------------------------------------------------
     def conv_args(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None,
-                  bn_bwd=None):
+                  bn_bwd=None, bn_fin: Optional[BnFin] = None):
         N, H, W, C = x.shape
         K, R, S, C2 = w.shape
         N2, P, Q, K2 = y.shape
@@ -180,6 +204,19 @@ class HipBackend(_Common):
             assert bx.shape == y.shape
             a.bn_x, a.bn_scale, a.bn_shift = bx.data_ptr(), bsc.data_ptr(), bsh.data_ptr()
             a.bn_mean, a.bn_invstd = bmu.data_ptr(), bis.data_ptr()
+        if bn_fin is not None:
+            assert stats is not None and bn_fin.counters.dtype == torch.int32 and bn_fin.counters.numel() >= (K + 63) // 64
+            f = bn_fin
+            a.fin_cnt = f.counters.data_ptr()
+            a.fin_count, a.fin_eps, a.fin_momentum = float(f.count), float(f.eps), float(f.momentum)
+            a.fin_gamma = f.gamma.data_ptr()
+            if bn_bwd is not None:
+                a.fin_dgamma, a.fin_dbeta, a.fin_coef = f.dgamma.data_ptr(), f.dbeta.data_ptr(), f.coef.data_ptr()
+            else:
+                a.fin_beta = f.beta.data_ptr()
+                a.fin_run_mean, a.fin_run_var = _ptr(f.run_mean), _ptr(f.run_var)
+                a.fin_scale, a.fin_shift = f.scale.data_ptr(), f.shift.data_ptr()
+                a.fin_mean, a.fin_invstd = f.mean.data_ptr(), f.invstd.data_ptr()
         a.cfg = self.forced_cfg if self.forced_cfg is not None else self.conv_cfg.get(self.conv_key(a), -1)
         return a
 
@@ -216,6 +253,7 @@ class HipBackend(_Common):
             t.residual = None
         if a.stats is not None:
             t.stats = st.data_ptr()
+        t.fin_cnt = None  # timing runs must not finalize (moving averages) the live BN
         best, best_t = 100, float("inf")
         s = self.stream()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -238,10 +276,12 @@ class HipBackend(_Common):
         self.tune_log.append((key, best, round(best_t * 1e3, 1)))
         return best
 
-    def conv_fwd(self, x, w, y, g, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None, bn_bwd=None):
+    def conv_fwd(self, x, w, y, g, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None, bn_bwd=None,
+                 bn_fin: Optional[BnFin] = None):
         """y = conv(x) (+ residual); optional BN statistics of y, or (bn_bwd = (x_bn, scale, shift,
-        mean, invstd)) the fused BN-backward reduction with ReLU-masked output."""
-        self.launch_conv(self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd))
+        mean, invstd)) the fused BN-backward reduction with ReLU-masked output; bn_fin finalizes
+        that BN in the same launch."""
+        self.launch_conv(self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd, bn_fin))
 
     WGRAD_TARGET_BLOCKS = int(os.environ.get("DRN_WGRAD_TARGET_BLOCKS", "512"))  # measured: 512 > 384, 640, 1024
     WGRAD_MIN_STEPS = int(os.environ.get("DRN_WGRAD_MIN_STEPS", "8"))
@@ -543,7 +583,18 @@ class RefBackend(_Common):
         return None
 
     def conv_fwd(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None,
-                 bn_bwd=None):
+                 bn_bwd=None, bn_fin: Optional[BnFin] = None):
+        self._conv_fwd(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd)
+        if bn_fin is not None:
+            f, G = bn_fin, stats.numel() // (2 * w.shape[0])
+            if bn_bwd is not None:
+                self.bn_finalize_bwd(stats, G, f.count, f.gamma, bn_bwd[4], f.dgamma, f.dbeta, f.coef)
+            else:
+                self.bn_finalize(stats, G, f.count, f.gamma, f.beta, f.run_mean, f.run_var, f.scale, f.shift, f.mean,
+                                 f.invstd, f.momentum, f.eps, update_running=f.run_mean is not None)
+
+    def _conv_fwd(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None,
+                  bn_bwd=None):
         K, R, S, C = w.shape
         _, P, Q, _ = y.shape
         if out_map is not None:

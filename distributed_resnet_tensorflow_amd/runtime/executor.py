@@ -29,7 +29,7 @@ from typing import Callable, List, Optional
 import torch
 
 from ..models.spec import Block, BN, Conv, NetSpec
-from ..ops.backend import ConvGeom, OutMap, dgrad_geom, tflip_desc, tflip_table
+from ..ops.backend import BnFin, ConvGeom, OutMap, dgrad_geom, tflip_desc, tflip_table
 from .params import ParamStore
 
 BN_DECAY = 0.997     # reference resnet_model_official.py:37
@@ -56,6 +56,10 @@ class BNState:
     act: Optional[torch.Tensor] = None     # materialised relu(bn(src)) (materialize_bn mode)
     bacc: Optional[torch.Tensor] = None    # backward sums [R][2][C] (sum g, sum g*xhat)
     bG: int = 1                            # replicas of bacc
+    fin_f: Optional[torch.Tensor] = None   # int32 arrival counters of the fused forward finalize
+    fin_b: Optional[torch.Tensor] = None   # ... and of the fused backward finalize
+    fin_done: bool = False                 # this step's forward finalize ran inside the producer conv
+    bfin_done: bool = False                # this step's backward finalize ran inside the dgrad
 
     @property
     def ss(self):
@@ -118,6 +122,11 @@ class Executor:
         # (measured: a win in the backward apply, a loss in the forward apply, whose per-thread
         # finalize prologue costs more than the separate C-thread finalize launch)
         self.fuse_finalize = os.environ.get("DRN_FUSE_BN_FINALIZE", "0") == "1"
+        # BN finalize inside the conv producing the statistics (last-arriving workgroup per
+        # channel column, DRN_FUSE_BN_FIN=1): removes ~100 small finalize launches per ImageNet
+        # step, but every workgroup must then wait for its atomics and a counter round trip
+        # before it retires -- measured 12.85 ms vs 11.78 ms per ResNet-50 step, so off
+        self.fuse_fin = os.environ.get("DRN_FUSE_BN_FIN", "0") == "1" and not self.deterministic
         self.fuse_finalize_fwd = os.environ.get("DRN_FUSE_BN_FINALIZE_FWD", "0") == "1"
         self.device = torch.device(device)
         self.wd, self.mom = weight_decay, momentum
@@ -215,11 +224,28 @@ class Executor:
         carved from the per-step-cleared arena."""
         R = self._det_replicas(M, C) if self.deterministic else self.stats_rep
         n = (2 * C * R + 15) // 16 * 16
-        if self._arena_off + n > self.stats_arena.numel():
+        if self._arena_off + n > self._arena_cap:
             raise RuntimeError("statistics arena exhausted")
         t = self.stats_arena[self._arena_off:self._arena_off + 2 * C * R].view(R, 2, C)
         self._arena_off += n
         return t, R
+
+    def _fin_counters(self) -> torch.Tensor:
+        t = self._fin_words[self._fin_off:self._fin_off + 64]
+        self._fin_off += 64
+        assert t.numel() == 64, "fused-finalize counter arena exhausted"
+        return t
+
+    def _fin_fwd(self, stats, train: bool):
+        """The BnFin that lets the conv producing `stats` finalize the BN consuming them."""
+        if not (train and self.fuse_fin) or stats is None:
+            return None
+        b = self._bn_by_stats.get(stats.data_ptr())
+        if b is None:
+            return None
+        b.fin_done = True
+        return BnFin(b.fin_f, b.rows, b.gamma, beta=b.beta, run_mean=b.run_mean, run_var=b.run_var, scale=b.scale,
+                     shift=b.shift, mean=b.mean, invstd=b.invstd, momentum=BN_DECAY, eps=BN_EPSILON)
 
     def _alloc(self):
         sp, N = self.spec, self.N
@@ -232,7 +258,13 @@ class Executor:
             arena = 64 + sum(2 * ((2 * c * self._det_replicas(m, c) + 15) // 16 * 16) for m, c in self._bn_shapes())
         else:
             arena = sum(2 * ((2 * c * self.stats_rep + 15) // 16 * 16) for c in all_c) + 64
-        self.stats_arena = self._f32(arena)
+        # + the arrival counters of the fused finalizes (64 per BN and direction), cleared with
+        # the statistics by the same per-step fill
+        n_bn = len(all_c) + 1
+        self._arena_cap = arena
+        self.stats_arena = self._f32(arena + 2 * 64 * n_bn)
+        self._fin_words = self.stats_arena[arena:].view(torch.int32)
+        self._fin_off = 0
         self._arena_off = 0
         wt_descs, wt_off = [], 0
         self.stem_op, wt_off = self._conv_op(sp.stem, wt_descs, wt_off)
@@ -312,6 +344,8 @@ class Executor:
                     b.act = self._act(*b.src.shape)
         for b in [b for bp in self.blocks for b in bp.bn] + [self.final_bn]:
             b.bacc, b.bG = self._stats_for(b.rows, b.bn.c)
+            b.fin_f, b.fin_b = self._fin_counters(), self._fin_counters()
+        self._bn_by_stats = {b.stats.data_ptr(): b for b in [b for bp in self.blocks for b in bp.bn] + [self.final_bn]}
         self.last_out = x
         C, ncls = sp.final_c, sp.num_classes
         self.pooled = self._f32(N, C)
@@ -369,6 +403,11 @@ class Executor:
     # forward
     # ------------------------------------------------------------------------------------------
     def _bn_fwd(self, b: BNState, train: bool):
+        if train and b.fin_done:  # finalized by the producing conv
+            b.fin_done = False
+            if b.act is not None:
+                self.be.bn_apply(b.src, b.act, b.scale, b.shift, relu=True)
+            return
         if train and b.act is not None and self.fuse_finalize_fwd and b.G == 1:
             self.be.bn_apply_stats(b.src, b.act, b.stats, b.rows, b.gamma, b.beta, b.run_mean, b.run_var, b.scale,
                                    b.shift, b.mean, b.invstd, BN_DECAY, BN_EPSILON, relu=True)
@@ -393,7 +432,8 @@ class Executor:
         if train:
             be.zero_(self.stats_arena)
         st = self.stem_op
-        be.conv_fwd(self.images, st.w, self.stem_out, st.geom, stats=self.stem_stats if train else None)
+        be.conv_fwd(self.images, st.w, self.stem_out, st.geom, stats=self.stem_stats if train else None,
+                    bn_fin=self._fin_fwd(self.stem_stats, train))
         if sp.maxpool:
             ph = sp.pool_hw
             pad = max((ph - 1) * 2 + 3 - sp.stem_hw, 0) // 2
@@ -439,10 +479,10 @@ class Executor:
             if last:
                 res = bp.sc if bp.proj is not None else bp.x
                 be.conv_fwd(xin, op.w, bp.out, op.geom, in_bn=pro, residual=res,
-                            stats=bp.out_stats if train else None)
+                            stats=bp.out_stats if train else None, bn_fin=self._fin_fwd(bp.out_stats, train))
             else:
                 be.conv_fwd(xin, op.w, bp.hs[i], op.geom, in_bn=pro,
-                            stats=bn[i + 1].stats if train else None)
+                            stats=bn[i + 1].stats if train else None, bn_fin=self._fin_fwd(bn[i + 1].stats, train))
                 self._bn_fwd(bn[i + 1], train)
 
     # ------------------------------------------------------------------------------------------
@@ -462,6 +502,10 @@ class Executor:
         if not reduced:
             G = be.bn_bwd_reduce(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, part)
         coef = self.bn_coef[:3 * b.bn.c]
+        if b.bfin_done:  # finalized by the producing data-gradient conv
+            b.bfin_done = False
+            be.bn_bwd_apply(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, coef, add, dx, relu=not reduced)
+            return
         if self.fuse_finalize and G == 1:
             be.bn_bwd_apply_stats(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, part, M, b.gamma,
                                   b.dgamma, b.dbeta, add, dx, coef=coef, relu=not reduced)
@@ -509,13 +553,19 @@ class Executor:
         covering every dx element) the epilogue also performs that BN's backward reduction."""
         if not accumulate and not op.full_cover:
             self.be.zero_(dx)
-        fuse = None
+        fuse = fin = None
         if bn is not None:
             assert op.full_cover
             fuse = (bn_x, bn.scale, bn.shift, bn.mean, bn.invstd)
-        for ph in op.dg:
+            if self.fuse_fin:  # the last phase launch finalizes the BN backward too
+                C = bn.bn.c
+                fin = BnFin(bn.fin_b, bn.rows, bn.gamma, dgamma=bn.dgamma, dbeta=bn.dbeta, coef=self.bn_coef[:3 * C])
+                bn.bfin_done = True
+        last = len(op.dg) - 1
+        for k, ph in enumerate(op.dg):
             self.be.conv_fwd(dy, ph.wt, dx, ph.geom, residual=dx if accumulate else None, out_map=ph.out_map,
-                             stats=bn.bacc if fuse is not None else None, bn_bwd=fuse)
+                             stats=bn.bacc if fuse is not None else None, bn_bwd=fuse,
+                             bn_fin=fin if k == last else None)
 
     def _block_bwd(self, bp: BlockPlan, bufs, cur: int) -> int:
         """Back-propagates one block; bufs[cur] holds d(block output). Returns the index of the

@@ -434,3 +434,59 @@ def test_cifar_augment(hip, ref):
     hip.cifar_augment(raw.cuda(), params.cuda(), o, 4)
     torch.cuda.synchronize()
     assert rel(o, o_ref) < 1e-2
+
+
+@pytest.mark.parametrize("cfg", [100, 0, 3, 10, 15, 17])
+@pytest.mark.parametrize("bwd", [False, True])
+def test_conv_fused_bn_finalize(hip, ref, cfg, bwd):
+    """The last-arriving workgroup of each channel column finalizes the BN (forward: scale /
+    shift / mean / invstd + moving averages; backward: dgamma, dbeta, coef) inside the conv,
+    matching the separate finalize; the arrival counters are re-armed for the next launch."""
+    from distributed_resnet_tensorflow_amd.ops.backend import BnFin
+    torch.manual_seed(12)
+    N, H, C, K = 8, 28, 64, 320          # K = 320: partial channel columns for BC = 128 / 256
+    x = bf(torch.randn(N, H, H, C))
+    w = bf(torch.randn(K, 3, 3, C) * 0.05)
+    g = ConvGeom(1, 1, 1)
+    count = float(N * H * H)
+    xb = bf(torch.randn(N, H, H, K))
+    sc, sh = torch.rand(K) + 0.5, torch.randn(K) * 0.3
+    mu, istd = torch.randn(K) * 0.1, torch.rand(K) + 0.5
+    gamma, beta = torch.rand(K) + 0.5, torch.randn(K) * 0.1
+    rm0, rv0 = torch.randn(K) * 0.1, torch.rand(K) + 0.5
+
+    def run(be, dev, dt):
+        t = lambda v: v.to(dev)
+        y = torch.zeros(N, H, H, K, dtype=dt, device=dev)
+        rep = getattr(be, "stats_replicas", 1)
+        st = torch.zeros(rep, 2, K, device=dev)
+        outs = {k: torch.zeros(K, device=dev) for k in ("scale", "shift", "mean", "invstd", "dgamma", "dbeta")}
+        outs["coef"] = torch.zeros(3 * K, device=dev)
+        outs["run_mean"], outs["run_var"] = t(rm0.clone()), t(rv0.clone())
+        cnt = torch.zeros(64, dtype=torch.int32, device=dev)
+        if bwd:
+            fin = BnFin(cnt, count, t(gamma), dgamma=outs["dgamma"], dbeta=outs["dbeta"], coef=outs["coef"])
+            bb = (t(xb) if dev == "cuda" else xb.float(), t(sc), t(sh), t(mu), t(istd))
+        else:
+            fin = BnFin(cnt, count, t(gamma), beta=t(beta), run_mean=outs["run_mean"], run_var=outs["run_var"],
+                        scale=outs["scale"], shift=outs["shift"], mean=outs["mean"], invstd=outs["invstd"])
+            bb = None
+        xx, ww = (x.cuda(), w.cuda()) if dev == "cuda" else (x.float(), w.float())
+        if dev == "cuda":
+            a = be.conv_args(xx, ww, y, g, stats=st, bn_bwd=bb, bn_fin=fin)
+            a.cfg = cfg
+            for _ in range(2):   # second launch: the counters must have been re-armed
+                st.zero_()       # (the executor clears the statistics arena once per step)
+                be.launch_conv(a)
+            torch.cuda.synchronize()
+            assert int(cnt.abs().sum()) == 0, "arrival counters not re-armed"
+        else:
+            for _ in range(2):
+                be.conv_fwd(xx, ww, y, g, stats=st, bn_bwd=bb, bn_fin=fin)
+        return {k: v.float().cpu() for k, v in outs.items()}
+
+    got = run(hip, "cuda", torch.bfloat16)
+    exp = run(ref, "cpu", torch.float32)   # (the reference finalize clears its accumulator itself)
+    keys = ("dgamma", "dbeta", "coef") if bwd else ("scale", "shift", "mean", "invstd", "run_mean", "run_var")
+    for k in keys:
+        assert rel(got[k], exp[k]) < 2e-2, (k, rel(got[k], exp[k]))
