@@ -131,6 +131,12 @@ class Executor:
         self.device = torch.device(device)
         self.wd, self.mom = weight_decay, momentum
         self.is_hip = backend.name == "hip"
+        # weight gradients on a second HIP stream (DRN_WGRAD_STREAM=1): every wgrad (+ its split-K
+        # reduction) only feeds the optimizer, so it runs concurrently with the data-gradient /
+        # BN-backward chain of the critical path; events guard the gradient buffers it reads
+        self.side = torch.cuda.Stream(self.device) if (self.is_hip and
+                                                       os.environ.get("DRN_WGRAD_STREAM", "1") == "1") else None
+        self._pending = {}
         # BN-apply+ReLU either fused into every consuming conv's load prologue (recomputed by the
         # forward conv, the projection conv and both weight-gradient convs) or materialised once
         # per BN by a streaming kernel (one extra read+write of the tensor, no per-element VALU
@@ -529,24 +535,76 @@ class Executor:
             self.grad_ready(self.P.by_name[f"{fb.bn.name}/gamma"].offset)
         bufs = [self.g_a, self.g_b, self.g_c]
         cur = 0  # index of the buffer holding d_out
+        self._pending.clear()
+        lagged = None  # (lo, side event) of the previous block: reported one block late, so the
+        #               main stream waits on weight gradients that have (almost surely) finished
         for bp in reversed(self.blocks):
             cur = self._block_bwd(bp, bufs, cur)
             if self.check_nan:
                 self._check(self._view(bufs[cur], bp.x), f"input gradient of block {bp.blk.stage}.{bp.blk.index}")
             if self.grad_ready is not None:
-                self.grad_ready(bp.grad_lo)
+                if self.side is None:
+                    self.grad_ready(bp.grad_lo)
+                else:
+                    if lagged is not None:
+                        self._join(lagged[1])
+                        self.grad_ready(lagged[0])
+                    lagged = (bp.grad_lo, self._side_mark())
         d_x0 = self._view(bufs[cur], self.blocks[0].x)
         st = self.stem_op
         if sp.maxpool:
             d_stem = self._view(bufs[(cur + 1) % 3], self.stem_out)
+            self._claim(bufs[(cur + 1) % 3])
             ph = sp.pool_hw
             pad = max((ph - 1) * 2 + 3 - sp.stem_hw, 0) // 2
             be.maxpool_bwd(d_x0, self.pool_arg, d_stem, 3, 2, pad, pad)
         else:
             d_stem = d_x0
-        be.conv_wgrad(self.images, d_stem, st.dw, st.geom, ws=self.wgrad_ws)
+        self._wgrad(self.images, d_stem, st.dw, st.geom)
+        self._join()
         if self.grad_ready is not None:
+            if lagged is not None:
+                self.grad_ready(lagged[0])
             self.grad_ready(0)
+
+    # -- weight gradients on the side stream ---------------------------------------------------------
+    def _wgrad(self, x, dy, dw, geom, in_bn=None, dy_buf=None):
+        if self.side is None:
+            self.be.conv_wgrad(x, dy, dw, geom, in_bn=in_bn, ws=self.wgrad_ws)
+            return
+        main = torch.cuda.current_stream(self.device)
+        self.side.wait_stream(main)                      # x and dy are complete
+        with torch.cuda.stream(self.side):
+            self.be.conv_wgrad(x, dy, dw, geom, in_bn=in_bn, ws=self.wgrad_ws)
+        if dy_buf is not None:                           # the main stream must not overwrite dy early
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+            self._pending[id(dy_buf)] = ev
+
+    def _claim(self, buf):
+        """Before the main stream writes a rotating gradient buffer: wait for the side-stream
+        weight gradient still reading it."""
+        ev = self._pending.pop(id(buf), None)
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+
+    def _side_mark(self):
+        """Event after every weight gradient issued so far (None without a side stream)."""
+        if self.side is None:
+            return None
+        ev = torch.cuda.Event()
+        ev.record(self.side)
+        return ev
+
+    def _join(self, ev=None):
+        if self.side is None:
+            return
+        main = torch.cuda.current_stream(self.device)
+        if ev is None:
+            main.wait_stream(self.side)
+            self._pending.clear()
+        else:
+            main.wait_event(ev)
 
     def _dgrad(self, op: ConvOp, dy, dx, accumulate: bool, bn: Optional[BNState] = None, bn_x=None):
         """Data gradient of `op` into dx (+= when accumulate). With bn set (requires a launch set
@@ -580,7 +638,8 @@ class Executor:
             op, xin, b = bp.convs[i], ins[i], bp.bn[i]
             tgt = free[0] if dy_buf is not free[0] else free[1]
             a_in, pro = self._cin(b)
-            be.conv_wgrad(a_in, dy, op.dw, op.geom, in_bn=pro, ws=self.wgrad_ws)
+            self._wgrad(a_in, dy, op.dw, op.geom, in_bn=pro, dy_buf=dy_buf)
+            self._claim(tgt)
             da = self._view(tgt, xin)        # d relu(bn(xin))
             add = None
             fuse = self.fuse_bn_bwd and op.full_cover
@@ -588,7 +647,7 @@ class Executor:
                 # the projection's data gradient first, the main conv's accumulating one last so
                 # that its (full-cover, stride-1) epilogue can carry the fused BN reduction
                 pj = bp.proj
-                be.conv_wgrad(a_in, d_out, pj.dw, pj.geom, in_bn=pro, ws=self.wgrad_ws)
+                self._wgrad(a_in, d_out, pj.dw, pj.geom, in_bn=pro, dy_buf=bufs[cur])
                 self._dgrad(pj, d_out, da, accumulate=False)
                 self._dgrad(op, dy, da, accumulate=True, bn=b if fuse else None, bn_x=xin)
             else:
@@ -620,8 +679,10 @@ class Executor:
         BN moving statistics and gradients are restored afterwards (no training side effects)."""
         saved = self.P.bn_state.clone()
         hook, self.grad_ready = self.grad_ready, None
+        side, self.side = self.side, None  # time candidate kernels on an otherwise idle GPU
         self.forward(train=True)
         self.backward()
+        self.side = side
         self.grad_ready = hook
         self.P.bn_state.copy_(saved)
         self.P.grad.zero_()

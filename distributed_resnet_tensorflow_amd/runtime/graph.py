@@ -51,6 +51,10 @@ class SegmentedStepGraph:
         if engine.p2p is not None or engine.mode != "sync":
             raise ValueError("segmented graphs are for the synchronous RCCL/gloo engine")
         self.ex, self.eng, self.grad_scale = ex, engine, grad_scale
+        # a capture may end only when every forked stream has joined: the side-stream weight
+        # gradients (reported one block late) would straddle the cut points, so this step keeps
+        # them on the main stream
+        self._side, ex.side = ex.side, None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):

@@ -28,6 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default="128,56,64,256,1;128,56,256,64,1;128,14,256,1024,1;128,14,256,256,3")
     ap.add_argument("--cfg", type=int, default=-1)
+    ap.add_argument("--cfgs", default="", help="comma list: sweep configurations, print TB/s per variant")
     a = ap.parse_args()
     be = HipBackend()
     be.autotune = False
@@ -38,9 +39,25 @@ def main():
         y = torch.empty(N, H, H, K, device="cuda", dtype=torch.bfloat16)
         r = torch.randn(N, H, H, K, device="cuda").bfloat16()
         bx = torch.randn(N, H, H, K, device="cuda").bfloat16()
-        st = torch.zeros(2, K, device="cuda")
+        st = torch.zeros(be.stats_replicas, 2, K, device="cuda")
         v = [torch.rand(K, device="cuda") for _ in range(4)]
         g = ConvGeom(1, (R - 1) // 2, (R - 1) // 2)
+        xb, yb = x.numel() * 2, y.numel() * 2
+        nbytes = {"plain": xb + yb, "stats": xb + yb, "res": xb + 2 * yb, "res+stats": xb + 2 * yb, "bnbwd": xb + 2 * yb}
+        if a.cfgs:
+            for cfg in [int(c) for c in a.cfgs.split(",")]:
+                line = []
+                for name, kw in (("plain", {}), ("res+stats", dict(residual=r, stats=st))):
+                    args = be.conv_args(x, w, y, g, **kw)
+                    args.cfg = cfg
+                    if be.L.drn_conv_fwd2(__import__("ctypes").byref(args), be.zero_page.data_ptr(), be.stream()) != 0:
+                        line = None
+                        break
+                    t = timeit(lambda: be.launch_conv(args))
+                    line.append(f"{name} {t:7.1f}us {nbytes[name] / t / 1e6:5.2f}TB/s")
+                if line:
+                    print(f"N{N} {H}x{H} {C}->{K} k{R} cfg{cfg:3d}: " + "  ".join(line), flush=True)
+            continue
         res = {}
         for name, kw in (("plain", {}), ("stats", dict(stats=st)), ("res", dict(residual=r)),
                          ("res+stats", dict(residual=r, stats=st)),
