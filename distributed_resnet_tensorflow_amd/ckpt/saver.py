@@ -32,6 +32,30 @@ def _quote(s: str) -> str:
     return '"' + s.replace("\\", "\\\\").replace('"', '\\"') + '"'
 
 
+def write_graph_pbtxt(ckpt_dir: str, variables: List[tuple], meta: Optional[dict] = None) -> str:
+    """`graph.pbtxt` in checkpoint_dir (the chief's MonitoredTrainingSession writes the
+    GraphDef there at start). There is no TF graph here, so this is a text-format
+    GraphDef of the *variables* only -- one VariableV2 node per saved tensor with its TF dtype
+    and shape, plus global_step -- enough for tools that list a run's variables; it is not an
+    executable graph. variables: [(tf_name, tf_shape)]."""
+    def node(name, dtype, shape):
+        dims = "".join(f"\n          dim {{\n            size: {d}\n          }}" for d in shape)
+        return (f"node {{\n  name: {_quote(name)}\n  op: \"VariableV2\"\n"
+                f"  attr {{\n    key: \"dtype\"\n    value {{\n      type: {dtype}\n    }}\n  }}\n"
+                f"  attr {{\n    key: \"shape\"\n    value {{\n      shape {{{dims}\n      }}\n    }}\n  }}\n}}\n")
+    out = ["# drn: variables-only GraphDef (no executable graph); model: " +
+           json.dumps(meta or {}, sort_keys=True) + "\n"]
+    out += [node(n, "DT_FLOAT", shp) for n, shp in variables]
+    out.append(node("global_step", "DT_INT64", ()))
+    out.append("versions {\n  producer: 24\n}\n")
+    path = os.path.join(ckpt_dir, "graph.pbtxt")
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        f.write("".join(out))
+    os.replace(tmp, path)
+    return path
+
+
 def write_state(ckpt_dir: str, latest: str, all_paths: List[str]):
     lines = [f"model_checkpoint_path: {_quote(latest)}"] + \
             [f"all_model_checkpoint_paths: {_quote(p)}" for p in all_paths]

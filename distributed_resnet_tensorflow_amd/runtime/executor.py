@@ -236,6 +236,10 @@ class Executor:
         self._arena_off += n
         return t, R
 
+    def all_bn_states(self) -> List[BNState]:
+        """Every BatchNorm of the network in TF creation order."""
+        return [b for bp in self.blocks for b in bp.bn] + [self.final_bn]
+
     def _fin_counters(self) -> torch.Tensor:
         t = self._fin_words[self._fin_off:self._fin_off + 64]
         self._fin_off += 64

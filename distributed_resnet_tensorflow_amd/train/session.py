@@ -15,7 +15,7 @@ from typing import Callable, List, Optional
 
 import torch
 
-from ..ckpt.saver import Saver, latest_checkpoint
+from ..ckpt.saver import Saver, latest_checkpoint, write_graph_pbtxt
 from ..ops.backend import HipBackend, RefBackend
 from ..parallel.engine import DataParallelEngine
 from ..runtime.executor import Executor
@@ -59,6 +59,12 @@ class TrainingSession:
         self.world = cluster.world
         self.ckpt_dir = checkpoint_dir
         self.saver = Saver(checkpoint_dir, max_to_keep) if (checkpoint_dir and cluster.is_chief) else None
+        if self.saver is not None:
+            os.makedirs(checkpoint_dir, exist_ok=True)
+            tf_vars = [(sl.name, tuple(sl.tf_shape)) for sl in self.ex.P.slots]
+            tf_vars += [(f"{b.bn.name}/{k}", (b.bn.c,)) for b in self.ex.all_bn_states()
+                        for k in ("moving_mean", "moving_variance")]
+            write_graph_pbtxt(checkpoint_dir, tf_vars, self.meta)
         self.data_state = {}
         self.restored_from = None
         self._restore()

@@ -36,6 +36,8 @@ def test_single_train_eval_resume(cifar_dir, tmp_path):
     r = run(["resnet_single.py", "--train_steps=12"] + common)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "step = 10" in r.stdout and os.path.exists(os.path.join(ck, "model.ckpt-12.index"))
+    g = open(os.path.join(ck, "graph.pbtxt")).read()   # SURVEY §2.11 artifact (variables-only GraphDef)
+    assert 'name: "conv2d/kernel"' in g and 'name: "global_step"' in g and "moving_variance" in g
     r = run(["resnet_cifar_eval.py", "--mode=eval", "--eval_once=True", f"--eval_data_path={cifar_dir}",
              f"--log_root={ck}", f"--eval_dir={ev}", "--resnet_size=8", "--eval_batch_count=2"])
     assert r.returncode == 0 and "precision:" in r.stdout, r.stdout + r.stderr
