@@ -101,6 +101,7 @@ _SIGS = {
     "drn_vgg_preprocess": ([c_p, c_p, c_p, c_int, c_int, c_int, c_f, c_f, c_f, c_p], c_int),
     "drn_p2p_signal": ([c_p, c_int, c_p], c_int),
     "drn_p2p_reduce": ([c_p, c_int, c_p], c_int),
+    "drn_p2p_reduce2": ([c_p, c_int, c_p], c_int),
     "drn_p2p_wait": ([c_p, c_p, c_p], c_int),
     "drn_p2p_args_size": ([], c_int),
     "drn_synthetic_images": ([c_p, c_i64, ctypes.c_uint32, c_p], c_int),

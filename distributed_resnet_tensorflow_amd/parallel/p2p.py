@@ -5,14 +5,17 @@ all-reduce pays W-1 latency-bound steps per bucket; here each GPU maps every pee
 buffer once (hipIpcGetMemHandle / hipIpcOpenMemHandle, handles exchanged over the existing
 process group) and reduces a bucket in a single kernel that reads all peers concurrently. The
 synchronisation is device-side (epoch flags in IPC-mapped memory), so the whole step, comm
-included, stays capturable in one HIP graph. Large buckets are better served by RCCL; the
-engine chooses per bucket with --allreduce=auto.
+included, stays capturable in one HIP graph. Buckets of at least `two_shot_min_kb`
+(DRN_P2P_TWO_SHOT_MIN_KB, default 1024) use the two-shot form -- reduce-scatter of this rank's
+1/W shard, then all-gather of the peers' reduced shards from their (also IPC-mapped) output
+buffers -- which moves 2(W-1)/W of the bucket per GPU instead of (W-1)x.
 
 Limits: one node, <= 8 ranks, fp32 buckets whose element count is a multiple of 4.
 """
 from __future__ import annotations
 
 import ctypes
+import os
 import pickle
 
 import torch
@@ -22,6 +25,7 @@ from ..ops import _lib
 
 MAX_RANKS = 8
 N_SLOTS = 64          # ready slots (one per bucket) + the DONE slot 0
+N_KINDS = 3           # READY, DONE, RS_DONE (two-shot)
 _HIP = None
 
 
@@ -42,6 +46,7 @@ class P2PArgs(ctypes.Structure):
     _fields_ = [
         ("out", ctypes.c_void_p),
         ("inp", ctypes.c_void_p * MAX_RANKS),
+        ("out_peer", ctypes.c_void_p * MAX_RANKS),
         ("flags_local", ctypes.c_void_p),
         ("flags_peer", ctypes.c_void_p * MAX_RANKS),
         ("epoch", ctypes.c_void_p),
@@ -85,7 +90,7 @@ def _export(t: torch.Tensor):
 class P2PAllReduce:
     """Maps every rank's `grad` (and flag words) and reduces buckets of it into `out`."""
 
-    def __init__(self, grad: torch.Tensor, group=None):
+    def __init__(self, grad: torch.Tensor, group=None, two_shot_min_kb: int = -1):
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -97,31 +102,37 @@ class P2PAllReduce:
         self.grad = grad
         self.comm = torch.cuda.Stream(device=grad.device)
         dev = grad.device
+        self.two_shot_min = 1024 * (two_shot_min_kb if two_shot_min_kb >= 0 else
+                                    int(os.environ.get("DRN_P2P_TWO_SHOT_MIN_KB", "1024")))
         self.out = torch.zeros_like(grad)
-        self.flags = torch.zeros(N_SLOTS * 2 * MAX_RANKS, dtype=torch.int32, device=dev)
+        self.flags = torch.zeros(N_SLOTS * N_KINDS * MAX_RANKS, dtype=torch.int32, device=dev)
         self.epoch = torch.zeros(1, dtype=torch.int32, device=dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
-        mine = (_export(grad), _export(self.flags))
+        mine = (_export(grad), _export(self.flags), _export(self.out))
         allh = [None] * self.world
         dist.all_gather_object(allh, pickle.dumps(mine), group=group)
         self._opened = []
-        self.in_ptr, self.flag_ptr = [], []
+        self.in_ptr, self.flag_ptr, self.out_ptr = [], [], []
         h = _hip()
         for r, blob in enumerate(allh):
-            (gh, goff), (fh, foff) = pickle.loads(blob)
+            (gh, goff), (fh, foff), (oh, ooff) = pickle.loads(blob)
             if r == self.rank:
                 self.in_ptr.append(grad.data_ptr())
                 self.flag_ptr.append(self.flags.data_ptr())
+                self.out_ptr.append(self.out.data_ptr())
                 continue
-            ptrs = []
-            for hb, off in ((gh, goff), (fh, foff)):
-                hd = _IpcHandle.from_bytes(hb)
-                p = ctypes.c_void_p()
-                _check(h.hipIpcOpenMemHandle(ctypes.byref(p), hd, 1), "hipIpcOpenMemHandle")  # lazy peer access
-                self._opened.append(p.value)
-                ptrs.append(p.value + off)
+            ptrs, bases = [], {}   # buffers may share one allocation: open each handle once
+            for hb, off in ((gh, goff), (fh, foff), (oh, ooff)):
+                if hb not in bases:
+                    hd = _IpcHandle.from_bytes(hb)
+                    p = ctypes.c_void_p()
+                    _check(h.hipIpcOpenMemHandle(ctypes.byref(p), hd, 1), "hipIpcOpenMemHandle")  # lazy peer access
+                    self._opened.append(p.value)
+                    bases[hb] = p.value
+                ptrs.append(bases[hb] + off)
             self.in_ptr.append(ptrs[0])
             self.flag_ptr.append(ptrs[1])
+            self.out_ptr.append(ptrs[2])
         dist.barrier(group=group)
 
     def _args(self, lo: int, hi: int, slot: int) -> P2PArgs:
@@ -129,6 +140,7 @@ class P2PAllReduce:
         a.out = self.out.data_ptr() + lo * 4
         for r in range(self.world):
             a.inp[r] = self.in_ptr[r] + lo * 4
+            a.out_peer[r] = self.out_ptr[r] + lo * 4
             a.flags_peer[r] = self.flag_ptr[r]
         a.flags_local = self.flags.data_ptr()
         a.epoch = self.epoch.data_ptr()
@@ -159,7 +171,10 @@ class P2PAllReduce:
         # at most 128 workgroups: a reduce waiting for a slow peer must leave most CUs to this
         # rank's own backward kernels (which publish the later buckets the peers wait for)
         blocks = max(1, min(128, (hi - lo) // 4 // 256))
-        _lib.check(self.L.drn_p2p_reduce(ctypes.byref(a), blocks, self.comm.cuda_stream), "drn_p2p_reduce")
+        if (hi - lo) * 4 >= self.two_shot_min and self.world > 1:
+            _lib.check(self.L.drn_p2p_reduce2(ctypes.byref(a), blocks, self.comm.cuda_stream), "drn_p2p_reduce2")
+        else:
+            _lib.check(self.L.drn_p2p_reduce(ctypes.byref(a), blocks, self.comm.cuda_stream), "drn_p2p_reduce")
 
     def end_step(self):
         """All buckets reduced on this rank: tell the peers their inputs are free, and order the

@@ -38,6 +38,9 @@ def _make(spec, N, shard, seed, be=None):
 def _worker(rank, world, port, q, allreduce="rccl"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if allreduce == "p2p2":           # two-shot for every bucket
+            os.environ["DRN_P2P_TWO_SHOT_MIN_KB"] = "0"
+            allreduce = "p2p"
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2
@@ -78,10 +81,11 @@ def _worker(rank, world, port, q, allreduce="rccl"):
         q.put((rank, repr(e) + traceback.format_exc(), False))
 
 
-@pytest.mark.parametrize("allreduce", ["rccl", "p2p"])
+@pytest.mark.parametrize("allreduce", ["rccl", "p2p", "p2p2"])
 def test_dp_engine_gpu_two_ranks_one_device(allreduce):
     """rccl here means the engine's torch.distributed path (gloo on this one-GPU box); p2p is
-    the one-shot HIP-IPC kernel path (parallel/p2p.py) with its device-side epoch flags."""
+    the one-shot HIP-IPC kernel path (parallel/p2p.py) with its device-side epoch flags, p2p2
+    its two-shot (reduce-scatter + all-gather) form."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
