@@ -29,8 +29,14 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, h);
 }
 
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+// Two floats -> packed bf16 pair: one v_cvt_pk_bf16_f32 (RNE, NaN-preserving) instead of two
+// conversions plus a shift/or.
 __device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+  const f32x2_t f = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2_t));
 }
 
 // 8 bf16 held in a uint4 (16 bytes) <-> 8 floats.
@@ -52,6 +58,69 @@ __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+
+// 16-byte LDS read / write in inline asm, for LDS rewritten in place while LDS-DMAs of later
+// pipeline stages are still in flight: hipcc assumes a plain ds_read may alias a pending
+// global_load_lds and waits vmcnt(0) before its use, draining the pipeline. The caller orders
+// the reads with lds_wait_all() (and the writes with an lgkmcnt wait before its barrier).
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)reinterpret_cast<uintptr_t>(p); }
+
+__device__ __forceinline__ u32x4_t lds_read16(uint32_t addr) {
+  u32x4_t v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr));
+  return v;
+}
+
+__device__ __forceinline__ void lds_write16(uint32_t addr, u32x4_t v) {
+  asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+
+// s_waitcnt lgkmcnt(0) that the N registers it retires depend on (their consumers cannot be
+// scheduled above it).
+template <int N>
+__device__ __forceinline__ void lds_wait_all(u32x4_t (&v)[N]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(v[i]));
+}
+
+__device__ __forceinline__ void unpack8v(const u32x4_t& v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ u32x4_t pack8v(const float* f) {
+  u32x4_t v;
+  v.x = pack2bf(f[0], f[1]); v.y = pack2bf(f[2], f[3]);
+  v.z = pack2bf(f[4], f[5]); v.w = pack2bf(f[6], f[7]);
+  return v;
+}
+
+// relu(x * sc + sh) of N 16-byte bf16 pieces in LDS (v[] already read, lds_wait_all'ed), in
+// place; piece i is rewritten only when bit i of `ok` is set (pieces loaded from the zero page
+// stay zero). Ends with the lgkmcnt wait that completes the writes before the caller's barrier.
+template <int N, bool RELU>
+__device__ __forceinline__ void lds_bn_relu_store(const uint32_t (&addr)[N], const u32x4_t* v, uint32_t ok,
+                                                  const float* sc, const float* sh) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    if ((ok >> i) & 1u) {
+      float f[8];
+      unpack8v(v[i], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        f[j] = f[j] * sc[j] + sh[j];
+        if (RELU) f[j] = fmaxf(f[j], 0.f);
+      }
+      lds_write16(addr[i], pack8v(f));
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 // XCD-aware bijective remap of a linear workgroup id: consecutive logical tiles land on the

@@ -489,7 +489,14 @@ __device__ __forceinline__ int glds_swz(int row) {
   return ((row >> 2) & 1) << 1;
 }
 
-template <int BP, int BC, int WAVES_P, int NS, int NW = 4, bool PF = true, int BK = 64>
+// PRO: the input is the RAW pre-BN tensor and the kernel applies relu(x * in_scale + in_shift)
+// itself (pre-activation v2, reference resnet_model_official.py:113-119): after its counted
+// vmcnt wait every lane rewrites the 16-byte pieces its own LDS-DMAs landed for the stage
+// (ds_read_b128 -> 8 FMA + max -> ds_write_b128) before the stage's barrier, so no extra
+// barrier and no extra HBM pass; pieces read from the zero page (padding, rows past M) are
+// skipped and stay zero. The per-channel scale/shift are staged once into LDS behind the
+// pipeline stages. Used for 1x1 consumers, where it replaces a full streaming BN-apply pass.
+template <int BP, int BC, int WAVES_P, int NS, int NW = 4, bool PF = true, int BK = 64, bool PRO = false>
 __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a, const void* __restrict__ zero) {
   static_assert(BK == 64 || BK == 32, "k per stage");
   constexpr int NT = NW * 64;
@@ -602,6 +609,20 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   const int swz = glds_swz<BK>(fr);  // fragment row groups are 16-aligned: the swizzle bits are fr's
 
   const int T = Ktot / BK;
+  // fused-BN operands: [scale C][shift C] fp32 behind the stages (before any LDS-DMA is issued)
+  float* const ssl = reinterpret_cast<float*>(smem + NS * STAGE);
+  if constexpr (PRO) {
+    for (int c = tid * 4; c < C; c += NT * 4) {
+      *reinterpret_cast<float4*>(ssl + c) = *reinterpret_cast<const float4*>(a.in_scale + c);
+      *reinterpret_cast<float4*>(ssl + C + c) = *reinterpret_cast<const float4*>(a.in_shift + c);
+    }
+    __syncthreads();
+  }
+  // the lane's logical 16-byte chunk of the B rows it loads: identical for every piece i
+  // (RPG * NW rows apart leave the swizzle bits unchanged)
+  static_assert((RPG * NW) % 16 == 0, "piece stride must preserve the swizzle bits");
+  const int lcb = lpc ^ glds_swz<BK>(RPG * wave + lrow);
+  int xr = 0, xs = 0, xci = 0;  // tap / channel offset of the stage being transformed
   EpiPre<BP, BC, NT, PF> epre;
   epi_prefetch<BP, BC, NT, PF>(a, m0, c0, M, epre);  // residual / BN inputs in flight during the main loop
 #pragma unroll
@@ -612,6 +633,42 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
     // retire stage t: the stages issued after it (up to D-1) may stay in flight
     if (t + D - 1 < T) wait_vmcnt<G * (D - 1)>();
     else wait_vmcnt<0>();
+    if constexpr (PRO) {
+      char* sw = smem + (t % NS) * STAGE;
+      // one LDS round trip: this stage's scale/shift and the lane's landed pieces together
+      const uint32_t sp = lds_addr(ssl + xci + lcb * 8);
+      u32x4_t v[GB + 4];
+      v[GB] = lds_read16(sp);
+      v[GB + 1] = lds_read16(sp + 16);
+      v[GB + 2] = lds_read16(sp + 4 * C);
+      v[GB + 3] = lds_read16(sp + 4 * C + 16);
+      uint32_t pa[GB], ok = 0;
+#pragma unroll
+      for (int i = 0; i < GB; ++i) {
+        const int h = bh[i] + xr, w = bw[i] + xs;
+        ok |= ((unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) ? (1u << i) : 0u;
+        pa[i] = lds_addr(sw + (BC + RPG * NW * i + RPG * wave) * ROWB + lane * 16);
+        v[i] = lds_read16(pa[i]);
+      }
+      lds_wait_all<GB + 4>(v);
+      float sc[8], sh[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sc[j] = __uint_as_float(v[GB][j]);
+        sc[4 + j] = __uint_as_float(v[GB + 1][j]);
+        sh[j] = __uint_as_float(v[GB + 2][j]);
+        sh[4 + j] = __uint_as_float(v[GB + 3][j]);
+      }
+      lds_bn_relu_store<GB, true>(pa, v, ok, sc, sh);
+      xci += BK;
+      if (xci == C) {
+        xci = 0;
+        if (++xs == a.S) {
+          xs = 0;
+          ++xr;
+        }
+      }
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (t + D < T) issue((t + D) % NS);
@@ -637,14 +694,16 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   conv_epilogue<BP, BC, WP, WC, MI, MJ, NT, PF>(a, smem, acc, wp, wc, m0, c0, M, epre);
 }
 
-template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF, int BK>
+template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF, int BK, bool PRO>
 static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
   constexpr int LDS0 = NS * (BC + BP) * BK * 2;
-  constexpr int LDS = LDS0 > BP * BC * 4 ? LDS0 : BP * BC * 4;  // epilogue staging tile
+  const int lds_main = LDS0 + (PRO ? 8 * a->C : 0);                 // + fused-BN scale/shift
+  const int LDS = lds_main > BP * BC * 4 ? lds_main : BP * BC * 4;  // epilogue staging tile
+  if (LDS > 160 * 1024) return (int)hipErrorInvalidValue;
   static bool attr_set = false;
-  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS, NW, PF, BK>;
+  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS, NW, PF, BK, PRO>;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   const int M = a->N * a->P * a->Q;
@@ -659,9 +718,12 @@ static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t 
 template <int BP, int BC, int WAVES_P, int NS, int NW = 4, int BK = 64>
 static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
   if (a->C % BK) return (int)hipErrorInvalidValue;
-  if (a->residual != nullptr || a->bn_x != nullptr)
-    return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK>(a, zero, stream);
-  return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK>(a, zero, stream);
+  const bool pf = a->residual != nullptr || a->bn_x != nullptr;
+  if (a->in_scale != nullptr)
+    return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, true>(a, zero, stream)
+              : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, true>(a, zero, stream);
+  return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, false>(a, zero, stream)
+            : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false>(a, zero, stream);
 }
 
 // Tile configurations of the LDS-DMA kernel (index = DRN conv config id, also used by the
@@ -765,7 +827,7 @@ DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s);
 
 // Whether the LDS-DMA kernel family supports this convolution.
 DRN_API int drn_conv_glds_ok(const DrnConvFwdArgs* a) {
-  return a->C % 32 == 0 && a->dil == 1 && a->in_scale == nullptr;
+  return a->C % 32 == 0 && a->dil == 1 && (a->in_scale == nullptr || (a->C <= 4096 && a->relu_in != 0));
 }
 
 // Dispatch on a->cfg; zero = >= 16 bytes of device zeros (the LDS-DMA loader's padding source).

@@ -309,7 +309,12 @@ __device__ __forceinline__ void lgkm_fence(s16x4v (&a)[MI][2], s16x4v (&b)[MJ][2
   for (int j = 0; j < MJ; ++j) asm volatile("" : "+v"(b[j][0]), "+v"(b[j][1]));
 }
 
-template <int BKK, int BCO, int NS, int BP = 64>
+// PRO: x is the RAW pre-BN input of a conv whose forward applied relu(x * in_scale + in_shift)
+// in its prologue; the same transform is applied here to the patch image in LDS: after its
+// counted vmcnt wait each lane rewrites the pieces its own LDS-DMAs landed for the stage (the
+// lane's channels are fixed for the whole kernel, so scale/shift stay in registers) and the
+// stage's barrier publishes them. Zero-page pieces (padding, pixels past the split) stay zero.
+template <int BKK, int BCO, int NS, int BP = 64, bool PRO = false>
 __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a, const void* __restrict__ zero) {
   static_assert(BP == 32 || BP == 64, "pixels per stage");
   constexpr int KS = BP / 32;  // 32-deep MFMA k-slices per stage
@@ -357,6 +362,20 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
     ss = tap - rr * a.S;
   }
   const int roff = rr - a.pad_h, soff = ss - a.pad_w;
+  float psc[8], psh[8];  // fused BN of this lane's 8 input channels
+  if constexpr (PRO) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      psc[j] = kvalid ? a.in_scale[ci + j] : 0.f;
+      psh[j] = kvalid ? a.in_shift[ci + j] : 0.f;
+    }
+    // retire these loads now, before any LDS-DMA is in flight (a use inside the pipelined
+    // loop would otherwise make hipcc wait vmcnt(0) there every stage)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(psc[j]), "+v"(psh[j]));
+  }
+  static_assert(!PRO || IA * NS <= 32, "validity mask bits");
+  uint32_t okm = 0;  // PRO: bit (slot * IA + i) = piece i of that stage came from the image
   // ---- B (dY) loader ----
   const int brow = lane / LPB;
   int blc;
@@ -398,6 +417,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
       const bool ok = kvalid && am[i] < mend && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
       const uint32_t off = (uint32_t)(__mul24(an[i], HWC) + __mul24(h, WC) + __mul24(w, a.C) + ci);
       const void* src = ok ? (const void*)(xg + off) : zero;
+      if constexpr (PRO) {
+        const uint32_t bit = 1u << (slot * IA + i);
+        okm = ok ? (okm | bit) : (okm & ~bit);
+      }
       __builtin_amdgcn_global_load_lds((wg_gbl_void*)src, (wg_lds_void*)(st + r0 * WA), 16, 0, 0);
       am[i] += BP;
       aq[i] += dq;
@@ -446,6 +469,19 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
   for (int t = 0; t < T; ++t) {
     if (t + D - 1 < T) wg_wait_vmcnt<G * (D - 1)>();
     else wg_wait_vmcnt<0>();
+    if constexpr (PRO) {
+      const int slot = t % NS;
+      char* sw = smem + slot * STAGE;
+      uint32_t pa[IA];
+      u32x4_t v[IA];
+#pragma unroll
+      for (int i = 0; i < IA; ++i) {
+        pa[i] = lds_addr(sw + RIA * (wave + 4 * i) * WA + lane * 16);
+        v[i] = lds_read16(pa[i]);
+      }
+      lds_wait_all<IA>(v);
+      lds_bn_relu_store<IA, true>(pa, v, (okm >> (slot * IA)) & ((1u << IA) - 1u), psc, psh);
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (t + D < T) issue((t + D) % NS, mbeg + (t + D) * BP);
@@ -502,11 +538,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
     }
 }
 
-template <int BKK, int BCO, int NS, int BP = 64>
-static int launch_wgrad_glds(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
+template <int BKK, int BCO, int NS, int BP, bool PRO>
+static int launch_wgrad_glds_p(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
   constexpr int LDS = NS * (BP * BKK * 2 + BP * BCO * 2);
   static bool attr_set = false;
-  auto kern = conv_wgrad_glds_kernel<BKK, BCO, NS, BP>;
+  auto kern = conv_wgrad_glds_kernel<BKK, BCO, NS, BP, PRO>;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
@@ -516,6 +552,12 @@ static int launch_wgrad_glds(DrnConvWgradArgs* a, const void* zero, hipStream_t 
   const int nct = (a->K + BCO - 1) / BCO;
   hipLaunchKernelGGL(kern, dim3(nkt * nct, a->splits), dim3(256), LDS, s, *a, zero);
   return (int)hipGetLastError();
+}
+
+template <int BKK, int BCO, int NS, int BP = 64>
+static int launch_wgrad_glds(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
+  if (a->in_scale != nullptr) return launch_wgrad_glds_p<BKK, BCO, NS, BP, true>(a, zero, s);
+  return launch_wgrad_glds_p<BKK, BCO, NS, BP, false>(a, zero, s);
 }
 
 template <int NS, int BP>
@@ -608,7 +650,8 @@ DRN_API int drn_conv_wgrad(DrnConvWgradArgs* a, hipStream_t s) {
 DRN_API int drn_conv_wgrad2(DrnConvWgradArgs* a, const void* zero, int ns, hipStream_t s) {
   if ((a->C % 8) != 0 || (a->K % 8) != 0 || a->splits < 1 || (a->pix_per_split % 64) != 0)
     return (int)hipErrorInvalidValue;
-  if (a->in_scale != nullptr || zero == nullptr || ns == 0) return drn_conv_wgrad(a, s);
+  // the LDS-DMA kernels' fused BN prologue always applies the ReLU (pre-activation v2)
+  if (zero == nullptr || ns == 0 || (a->in_scale != nullptr && a->relu_in == 0)) return drn_conv_wgrad(a, s);
   return drn::dispatch_wgrad_glds(a, zero, ns, s);
 }
 

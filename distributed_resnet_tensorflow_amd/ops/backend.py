@@ -342,8 +342,6 @@ class HipBackend(_Common):
         """Pick the wgrad pipeline (0: register-staged, 2/3: LDS-DMA stages of 64 pixels, 4/5/6:
         2/3/4 stages of 32 pixels) by timing; the
         kernel only writes the split-K workspace (or the gradient slot, rewritten right after)."""
-        if a.in_scale is not None:
-            return 0
         st = self.stream()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         best, best_t = 2, float("inf")

@@ -138,12 +138,22 @@ class Executor:
                                                        os.environ.get("DRN_WGRAD_STREAM", "1") == "1") else None
         self._pending = {}
         # BN-apply+ReLU either fused into every consuming conv's load prologue (recomputed by the
-        # forward conv, the projection conv and both weight-gradient convs) or materialised once
-        # per BN by a streaming kernel (one extra read+write of the tensor, no per-element VALU
-        # work in the MFMA loops). Measured on MI355X the materialised form is faster.
+        # forward conv, the projection conv and both weight-gradient convs; the LDS-DMA kernels
+        # rewrite each landed stage in LDS before its barrier) or materialised once per BN by a
+        # streaming kernel (one extra read + write of the tensor). Policy "1x1" (default on the
+        # HIP backend): fuse where every consumer is a 1x1 conv -- each element is rewritten once
+        # per consuming tile, and the streaming pass it replaces is pure HBM traffic -- and
+        # materialise BNs feeding a 3x3 conv, whose 9 taps would transform every element 9 times.
+        # "all" materialises every BN, "none" fuses every BN (DRN_BN_MATERIALIZE).
         if materialize_bn is None:
-            materialize_bn = os.environ.get("DRN_FUSE_BN_PROLOGUE", "0") != "1"
-        self.materialize_bn = materialize_bn
+            policy = os.environ.get("DRN_BN_MATERIALIZE", "1x1" if self.is_hip else "all")
+            if os.environ.get("DRN_FUSE_BN_PROLOGUE") == "1":
+                policy = "none"
+        else:
+            policy = "all" if materialize_bn else "none"
+        assert policy in ("all", "1x1", "none"), policy
+        self.bn_policy = policy
+        self.materialize_bn = policy != "none"
         self.fdt = backend.acc_dtype
         self.P = params or ParamStore(spec, self.device, keep_bf16=self.is_hip, seed=seed, dtype=self.fdt)
         self.grad_ready: Optional[Callable[[int], None]] = None
@@ -348,9 +358,10 @@ class Executor:
         self.final_bn.stats, self.final_bn.G = x_stats, x_G
         self.final_bn.rows = x.numel() // sp.final_c
         self.final_bn.src = x
-        if self.materialize_bn:
-            for bp in self.blocks:
-                for b in bp.bn:
+        for bp in self.blocks:
+            for i, b in enumerate(bp.bn):
+                consumers = [bp.convs[i].conv] + ([bp.proj.conv] if i == 0 and bp.proj is not None else [])
+                if self.bn_policy == "all" or (self.bn_policy == "1x1" and any(c.k != 1 for c in consumers)):
                     b.act = self._act(*b.src.shape)
         for b in [b for bp in self.blocks for b in bp.bn] + [self.final_bn]:
             b.bacc, b.bG = self._stats_for(b.rows, b.bn.c)

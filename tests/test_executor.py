@@ -13,9 +13,22 @@ from distributed_resnet_tensorflow_amd.ops.backend import RefBackend
 from distributed_resnet_tensorflow_amd.runtime.executor import Executor
 
 
-def _check(spec, N, dtype, tol):
+def _check(spec, N, dtype, tol, policy=None):
     torch.manual_seed(0)
-    ex = Executor(spec, N, RefBackend(dtype=dtype), "cpu", seed=1)
+    if policy is not None:
+        import os
+        old = os.environ.get("DRN_BN_MATERIALIZE")
+        os.environ["DRN_BN_MATERIALIZE"] = policy
+    try:
+        ex = Executor(spec, N, RefBackend(dtype=dtype), "cpu", seed=1)
+    finally:
+        if policy is not None:
+            if old is None:
+                del os.environ["DRN_BN_MATERIALIZE"]
+            else:
+                os.environ["DRN_BN_MATERIALIZE"] = old
+    if policy is not None:
+        assert ex.bn_policy == policy
     ex.images.zero_()
     ex.images[..., :3] = torch.randn(N, spec.image_size, spec.image_size, 3, dtype=dtype)
     labels = torch.randint(0, spec.num_classes, (N,))
@@ -46,8 +59,11 @@ def test_imagenet_resnet18_fp32():
     _check(imagenet_resnet_v2(18, num_classes=10, image_size=64), 2, torch.float32, 1e-4)
 
 
-def test_imagenet_resnet50_fp64():
-    _check(imagenet_resnet_v2(50, num_classes=7, image_size=64), 2, torch.float64, 1e-9)
+@pytest.mark.parametrize("policy", ["all", "1x1", "none"])
+def test_imagenet_resnet50_fp64(policy):
+    """Every BN-apply placement (materialised / fused into 1x1 consumers / fused everywhere)
+    gives the oracle's gradients."""
+    _check(imagenet_resnet_v2(50, num_classes=7, image_size=64), 2, torch.float64, 1e-9, policy=policy)
 
 
 def test_sgd_step_matches_torch_momentum():

@@ -86,9 +86,11 @@ GLDS_CASES = [
 
 @pytest.mark.parametrize("case", GLDS_CASES)
 @pytest.mark.parametrize("cfg", list(range(23)))
-def test_conv_fwd_glds_configs(hip, ref, case, cfg):
+@pytest.mark.parametrize("pro", [False, True])
+def test_conv_fwd_glds_configs(hip, ref, case, cfg, pro):
     """Every tile/pipeline configuration of the LDS-DMA conv kernel vs the fp32 reference,
-    with residual add + BN statistics epilogue."""
+    with residual add + BN statistics epilogue; pro: the input is the raw pre-BN tensor and the
+    kernel applies relu(x * scale + shift) to each landed stage in LDS (padding stays zero)."""
     N, H, W, C, K, R, s, p = case
     torch.manual_seed(10 + cfg)
     P = out_size(H, R, s, p)
@@ -96,12 +98,14 @@ def test_conv_fwd_glds_configs(hip, ref, case, cfg):
     w = bf(torch.randn(K, R, R, C) * (2.0 / (R * R * C)) ** 0.5)
     res = bf(torch.randn(N, P, P, K))
     g = ConvGeom(stride=s, pad_h=p, pad_w=p)
+    in_bn = (torch.rand(C) + 0.5, torch.randn(C) * 0.5) if pro else None
     y_ref = torch.zeros(N, P, P, K)
     st_ref = torch.zeros(2 * K)
-    ref.conv_fwd(x.float(), w.float(), y_ref, g, residual=res.float(), stats=st_ref)
+    ref.conv_fwd(x.float(), w.float(), y_ref, g, in_bn=in_bn, residual=res.float(), stats=st_ref)
     y = torch.zeros(N, P, P, K, dtype=torch.bfloat16, device="cuda")
     st = torch.zeros(3, 2, K, device="cuda")  # 3 atomic-spreading replicas
-    a = hip.conv_args(x.cuda(), w.cuda(), y, g, residual=res.cuda(), stats=st)
+    a = hip.conv_args(x.cuda(), w.cuda(), y, g, residual=res.cuda(), stats=st,
+                      in_bn=None if in_bn is None else (in_bn[0].cuda(), in_bn[1].cuda()))
     assert hip.L.drn_conv_glds_ok(a) == 1 and a.stats_rep == 3
     a.cfg = cfg
     if C % 64 and cfg < 17:
@@ -218,22 +222,26 @@ WGRAD_GLDS_CASES = [
 
 @pytest.mark.parametrize("case", WGRAD_GLDS_CASES)
 @pytest.mark.parametrize("ns", [0, 2, 3, 4, 5, 6])
-def test_conv_wgrad_pipelines(hip, ref, case, ns):
-    """Register-staged (ns=0) and LDS-DMA (2/3 stages) weight-gradient kernels vs fp32."""
+@pytest.mark.parametrize("fused", [False, True])
+def test_conv_wgrad_pipelines(hip, ref, case, ns, fused):
+    """Register-staged (ns=0) and LDS-DMA (2/3 stages) weight-gradient kernels vs fp32;
+    fused: the patch operand is relu(x * scale + shift) of the raw input, applied in LDS."""
     N, H, W, C, K, R, s, p = case
     torch.manual_seed(7)
     P = out_size(H, R, s, p)
     x = bf(torch.randn(N, H, W, C))
     dy = bf(torch.randn(N, P, P, K))
     g = ConvGeom(stride=s, pad_h=p, pad_w=p)
+    in_bn = (torch.rand(C) + 0.5, torch.randn(C) * 0.5) if fused else None
     dw_ref = torch.zeros(K, R, R, C)
-    ref.conv_wgrad(x.float(), dy.float(), dw_ref, g)
+    ref.conv_wgrad(x.float(), dy.float(), dw_ref, g, in_bn=in_bn)
     dw = torch.zeros(K, R, R, C, device="cuda")
     ws = torch.zeros(max(1, hip.wgrad_ws_elems(N * P * P, K, R, R, C)), device="cuda")
     old = hip.forced_wgrad_ns
     hip.forced_wgrad_ns = ns
     try:
-        hip.conv_wgrad(x.cuda(), dy.cuda(), dw, g, ws=ws)
+        hip.conv_wgrad(x.cuda(), dy.cuda(), dw, g, ws=ws,
+                       in_bn=None if in_bn is None else (in_bn[0].cuda(), in_bn[1].cuda()))
     finally:
         hip.forced_wgrad_ns = old
     torch.cuda.synchronize()
