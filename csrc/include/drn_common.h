@@ -101,24 +101,45 @@ __device__ __forceinline__ u32x4_t pack8v(const float* f) {
   return v;
 }
 
-// relu(x * sc + sh) of N 16-byte bf16 pieces in LDS (v[] already read, lds_wait_all'ed), in
-// place; piece i is rewritten only when bit i of `ok` is set (pieces loaded from the zero page
-// stay zero). Ends with the lgkmcnt wait that completes the writes before the caller's barrier.
+typedef short s16x2_t __attribute__((ext_vector_type(2)));
+
+// relu(x * sc + sh) of 8 bf16 (one 16-byte piece), packed: per pair one v_pk_fma_f32, one
+// v_cvt_pk_bf16_f32 and the ReLU as ONE v_pk_max_i16 against 0 on the packed result (a bf16
+// with its sign bit set is a negative int16; -0 becomes +0). sc2/sh2 hold the 4 channel pairs.
+template <bool RELU>
+__device__ __forceinline__ u32x4_t bn_relu_piece(const u32x4_t& v, const f32x2_t* sc2, const f32x2_t* sh2) {
+  u32x4_t o;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const uint32_t u = v[p];
+    f32x2_t f = {__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+    f = f * sc2[p] + sh2[p];
+    uint32_t r = __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2_t));
+    if (RELU) {
+      const s16x2_t z = {0, 0};
+      r = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2_t, r), z));
+    }
+    o[p] = r;
+  }
+  return o;
+}
+
+// The same for N pieces in LDS (v[] already read and lds_wait_all'ed), written back in place;
+// piece i keeps its (zero) contents unless bit i of `ok` is set -- pieces loaded from the zero
+// page stay zero. Branch-free. Ends with the lgkmcnt wait that completes the writes before the
+// caller's barrier.
 template <int N, bool RELU>
 __device__ __forceinline__ void lds_bn_relu_store(const uint32_t (&addr)[N], const u32x4_t* v, uint32_t ok,
-                                                  const float* sc, const float* sh) {
+                                                  const f32x2_t* sc2, const f32x2_t* sh2) {
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    if ((ok >> i) & 1u) {
-      float f[8];
-      unpack8v(v[i], f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        f[j] = f[j] * sc[j] + sh[j];
-        if (RELU) f[j] = fmaxf(f[j], 0.f);
-      }
-      lds_write16(addr[i], pack8v(f));
-    }
+    u32x4_t o = bn_relu_piece<RELU>(v[i], sc2, sh2);
+    const unsigned m = ((ok >> i) & 1u) ? 0xffffffffu : 0u;
+    o.x &= m;
+    o.y &= m;
+    o.z &= m;
+    o.w &= m;
+    lds_write16(addr[i], o);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }

@@ -57,7 +57,10 @@ struct DrnConvFwdArgs {
   // only the last launch carries it.
   unsigned* fin_cnt;
   float fin_count, fin_eps, fin_momentum;
-  int32_t fin_pad_;
+  // With a strided output map: 1 = the epilogue also stores zeros at the other phase positions
+  // of every output pixel (single-phase data gradient, e.g. a 1x1 stride-2 projection), so the
+  // output tensor needs no separate clearing pass.
+  int32_t out_fill;
   const float* fin_gamma;
   const float* fin_beta;
   float* fin_run_mean;

@@ -214,6 +214,21 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
         *reinterpret_cast<uint4*>(y + off) = pack8(f);
       } else {
         *reinterpret_cast<uint4*>(y + off) = o;
+        if (a.out_fill && a.out_stride > 1) {
+          // zeros at this pixel's sibling phase positions (single-phase strided output)
+          const int m = m0 + row;
+          const int pq = a.P * a.Q;
+          const int n = m / pq;
+          const int rem = m - n * pq;
+          const int i = rem / a.Q;
+          const int j = rem - i * a.Q;
+          for (int ph = 0; ph < a.out_stride; ++ph)
+            for (int pw = 0; pw < a.out_stride; ++pw) {
+              const int hh = i * a.out_stride + ph, ww = j * a.out_stride + pw;
+              if ((ph != a.out_oh || pw != a.out_ow) && hh < a.out_H && ww < a.out_W)
+                *reinterpret_cast<uint4*>(y + ((n * a.out_H + hh) * a.out_W + ww) * a.K + c) = make_uint4(0u, 0u, 0u, 0u);
+            }
+        }
         if (want_stats) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
@@ -651,15 +666,15 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
         v[i] = lds_read16(pa[i]);
       }
       lds_wait_all<GB + 4>(v);
-      float sc[8], sh[8];
+      f32x2_t sc2[4], sh2[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        sc[j] = __uint_as_float(v[GB][j]);
-        sc[4 + j] = __uint_as_float(v[GB + 1][j]);
-        sh[j] = __uint_as_float(v[GB + 2][j]);
-        sh[4 + j] = __uint_as_float(v[GB + 3][j]);
+      for (int q = 0; q < 2; ++q) {
+        sc2[2 * q] = f32x2_t{__uint_as_float(v[GB + q][0]), __uint_as_float(v[GB + q][1])};
+        sc2[2 * q + 1] = f32x2_t{__uint_as_float(v[GB + q][2]), __uint_as_float(v[GB + q][3])};
+        sh2[2 * q] = f32x2_t{__uint_as_float(v[GB + 2 + q][0]), __uint_as_float(v[GB + 2 + q][1])};
+        sh2[2 * q + 1] = f32x2_t{__uint_as_float(v[GB + 2 + q][2]), __uint_as_float(v[GB + 2 + q][3])};
       }
-      lds_bn_relu_store<GB, true>(pa, v, ok, sc, sh);
+      lds_bn_relu_store<GB, true>(pa, v, ok, sc2, sh2);
       xci += BK;
       if (xci == C) {
         xci = 0;

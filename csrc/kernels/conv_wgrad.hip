@@ -362,17 +362,17 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
     ss = tap - rr * a.S;
   }
   const int roff = rr - a.pad_h, soff = ss - a.pad_w;
-  float psc[8], psh[8];  // fused BN of this lane's 8 input channels
+  f32x2_t psc2[4], psh2[4];  // fused BN of this lane's 8 input channels (channel pairs)
   if constexpr (PRO) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      psc[j] = kvalid ? a.in_scale[ci + j] : 0.f;
-      psh[j] = kvalid ? a.in_shift[ci + j] : 0.f;
+    for (int p = 0; p < 4; ++p) {
+      psc2[p] = kvalid ? f32x2_t{a.in_scale[ci + 2 * p], a.in_scale[ci + 2 * p + 1]} : f32x2_t{0.f, 0.f};
+      psh2[p] = kvalid ? f32x2_t{a.in_shift[ci + 2 * p], a.in_shift[ci + 2 * p + 1]} : f32x2_t{0.f, 0.f};
     }
     // retire these loads now, before any LDS-DMA is in flight (a use inside the pipelined
     // loop would otherwise make hipcc wait vmcnt(0) there every stage)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(psc[j]), "+v"(psh[j]));
+    for (int p = 0; p < 4; ++p) asm volatile("" : "+v"(psc2[p]), "+v"(psh2[p]));
   }
   static_assert(!PRO || IA * NS <= 32, "validity mask bits");
   uint32_t okm = 0;  // PRO: bit (slot * IA + i) = piece i of that stage came from the image
@@ -480,7 +480,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
         v[i] = lds_read16(pa[i]);
       }
       lds_wait_all<IA>(v);
-      lds_bn_relu_store<IA, true>(pa, v, (okm >> (slot * IA)) & ((1u << IA) - 1u), psc, psh);
+      lds_bn_relu_store<IA, true>(pa, v, (okm >> (slot * IA)) & ((1u << IA) - 1u), psc2, psh2);
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");

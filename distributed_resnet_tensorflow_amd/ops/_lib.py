@@ -47,7 +47,7 @@ class DrnConvFwdArgs(ctypes.Structure):
         ("cfg", c_int), ("stats_rep", c_int),
         ("bn_x", c_p), ("bn_scale", c_p), ("bn_shift", c_p), ("bn_mean", c_p), ("bn_invstd", c_p),
         ("fin_cnt", c_p), ("fin_count", ctypes.c_float), ("fin_eps", ctypes.c_float),
-        ("fin_momentum", ctypes.c_float), ("fin_pad_", c_int),
+        ("fin_momentum", ctypes.c_float), ("out_fill", c_int),
         ("fin_gamma", c_p), ("fin_beta", c_p), ("fin_run_mean", c_p), ("fin_run_var", c_p),
         ("fin_scale", c_p), ("fin_shift", c_p), ("fin_mean", c_p), ("fin_invstd", c_p),
         ("fin_dgamma", c_p), ("fin_dbeta", c_p), ("fin_coef", c_p),

@@ -277,11 +277,16 @@ class HipBackend(_Common):
         return best
 
     def conv_fwd(self, x, w, y, g, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None, bn_bwd=None,
-                 bn_fin: Optional[BnFin] = None):
+                 bn_fin: Optional[BnFin] = None, out_fill: bool = False):
         """y = conv(x) (+ residual); optional BN statistics of y, or (bn_bwd = (x_bn, scale, shift,
         mean, invstd)) the fused BN-backward reduction with ReLU-masked output; bn_fin finalizes
-        that BN in the same launch."""
-        self.launch_conv(self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd, bn_fin))
+        that BN in the same launch. out_fill (strided out_map, single-phase output): the epilogue
+        also writes zeros at every other phase position, so y needs no separate clearing."""
+        a = self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd, bn_fin)
+        if out_fill:
+            assert out_map is not None and bn_bwd is None and residual is None, "out_fill: plain strided output only"
+            a.out_fill = 1
+        self.launch_conv(a)
 
     WGRAD_TARGET_BLOCKS = int(os.environ.get("DRN_WGRAD_TARGET_BLOCKS", "512"))  # measured: 512 > 384, 640, 1024
     WGRAD_MIN_STEPS = int(os.environ.get("DRN_WGRAD_MIN_STEPS", "8"))
@@ -581,8 +586,8 @@ class RefBackend(_Common):
         return None
 
     def conv_fwd(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None,
-                 bn_bwd=None, bn_fin: Optional[BnFin] = None):
-        self._conv_fwd(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd)
+                 bn_bwd=None, bn_fin: Optional[BnFin] = None, out_fill: bool = False):
+        self._conv_fwd(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd, out_fill)
         if bn_fin is not None:
             f, G = bn_fin, stats.numel() // (2 * w.shape[0])
             if bn_bwd is not None:
@@ -592,7 +597,7 @@ class RefBackend(_Common):
                                  f.invstd, f.momentum, f.eps, update_running=f.run_mean is not None)
 
     def _conv_fwd(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None,
-                  bn_bwd=None):
+                  bn_bwd=None, out_fill=False):
         K, R, S, C = w.shape
         _, P, Q, _ = y.shape
         if out_map is not None:
@@ -616,6 +621,8 @@ class RefBackend(_Common):
             stats.view(-1)[:K].add_(gg.sum(0))
             stats.view(-1)[K:2 * K].add_((gg * xh).sum(0))
         if sl is not None:
+            if out_fill:
+                y.zero_()
             y[sl] = out.to(y.dtype)
             return
         y.copy_(out)

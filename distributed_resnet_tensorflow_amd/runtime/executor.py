@@ -8,8 +8,9 @@ runtime/graph.py). There is no autograd tape: the backward of the pre-activation
 written out explicitly, which is what lets BatchNorm/ReLU be fused across kernel boundaries:
 
   forward, per conv: y = conv( relu(bn(x)) ) [+ shortcut]   -- BN-apply+ReLU in the load
-      prologue of the consuming conv (the normalised activation is never written to HBM),
-      residual add + the NEXT BN's partial statistics in the epilogue of the producing conv.
+      prologue of the consuming 1x1 convs (rewritten in LDS, never written to HBM) or, for BNs
+      feeding a 3x3 conv, materialised once by a streaming kernel (bn_policy); residual add +
+      the NEXT BN's partial statistics in the epilogue of the producing conv.
   backward, per conv: dgrad as a forward conv of dY with flipped/transposed weights (the
       projection-shortcut dgrad accumulates through the residual epilogue), wgrad recomputes
       relu(bn(x)) in its load prologue, BN-ReLU backward = reduce -> finalize -> apply (+ the
@@ -128,6 +129,8 @@ class Executor:
         # before it retires -- measured 12.85 ms vs 11.78 ms per ResNet-50 step, so off
         self.fuse_fin = os.environ.get("DRN_FUSE_BN_FIN", "0") == "1" and not self.deterministic
         self.fuse_finalize_fwd = os.environ.get("DRN_FUSE_BN_FINALIZE_FWD", "0") == "1"
+        # single-phase strided data gradients zero the other phases in their own epilogue
+        self.out_fill = os.environ.get("DRN_OUT_FILL", "1") == "1"
         self.device = torch.device(device)
         self.wd, self.mom = weight_decay, momentum
         self.is_hip = backend.name == "hip"
@@ -624,7 +627,11 @@ class Executor:
     def _dgrad(self, op: ConvOp, dy, dx, accumulate: bool, bn: Optional[BNState] = None, bn_x=None):
         """Data gradient of `op` into dx (+= when accumulate). With bn set (requires a launch set
         covering every dx element) the epilogue also performs that BN's backward reduction."""
-        if not accumulate and not op.full_cover:
+        # a single-phase strided data gradient (1x1 stride-2 projection) writes the zeros of the
+        # other phases from its own epilogue instead of a separate clearing pass over dx
+        fill = self.out_fill and not accumulate and not op.full_cover and len(op.dg) == 1 \
+            and op.dg[0].out_map is not None and bn is None
+        if not accumulate and not op.full_cover and not fill:
             self.be.zero_(dx)
         fuse = fin = None
         if bn is not None:
@@ -638,7 +645,7 @@ class Executor:
         for k, ph in enumerate(op.dg):
             self.be.conv_fwd(dy, ph.wt, dx, ph.geom, residual=dx if accumulate else None, out_map=ph.out_map,
                              stats=bn.bacc if fuse is not None else None, bn_bwd=fuse,
-                             bn_fin=fin if k == last else None)
+                             bn_fin=fin if k == last else None, out_fill=fill)
 
     def _block_bwd(self, bp: BlockPlan, bufs, cur: int) -> int:
         """Back-propagates one block; bufs[cur] holds d(block output). Returns the index of the

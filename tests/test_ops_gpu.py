@@ -137,6 +137,34 @@ def test_conv_glds_out_map(hip, ref):
         assert rel(y, y_ref) < 1e-2, cfg
 
 
+@pytest.mark.parametrize("cfg", [100, 0, 3, 6, 13, 18])
+@pytest.mark.parametrize("size", [5, 4])
+def test_conv_out_fill(hip, ref, cfg, size):
+    """Single-phase strided output (1x1 stride-2 projection data gradient) with out_fill: the
+    epilogue writes zeros at the other phase positions of a garbage-filled output (odd and even
+    output sizes)."""
+    torch.manual_seed(6)
+    N, C, K = 2, 64, 64
+    H = 2 * size - 1  # odd: the last phase row/column is cut off
+    P = (H + 1) // 2
+    x = bf(torch.randn(N, P, P, C))
+    w = bf(torch.randn(K, 1, 1, C) * 0.1)
+    om = OutMap(P=P, Q=P, stride=2, oh=0, ow=0)
+    y_ref = torch.full((N, H, H, K), 7.0)
+    ref.conv_fwd(x.float(), w.float(), y_ref, ConvGeom(1, 0, 0), out_map=om, out_fill=True)
+    assert float(y_ref[:, 1::2].abs().max()) == 0.0
+    y = torch.full((N, H, H, K), 7.0, dtype=torch.bfloat16, device="cuda")
+    old = hip.forced_cfg
+    hip.forced_cfg = cfg
+    try:
+        hip.conv_fwd(x.cuda(), w.cuda(), y, ConvGeom(1, 0, 0), out_map=om, out_fill=True)
+    finally:
+        hip.forced_cfg = old
+    torch.cuda.synchronize()
+    assert rel(y, y_ref) < 1e-2, cfg
+    assert float(y.float()[:, :, 1::2].abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("cfg", [100, 0, 3, 6])
 def test_conv_fused_bn_bwd_reduce(hip, ref, cfg):
     """Data-gradient conv with the fused BN-backward epilogue (ReLU mask + sum g, sum g*xhat)."""
