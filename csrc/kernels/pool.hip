@@ -86,6 +86,68 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restri
   }
 }
 
+// Stride-2 backward, one thread per 2x2 block of input pixels x 8 channels: the (at most 2x2)
+// windows touching the block are each read once (dy + argmax) and scattered to the block's 4
+// pixels in registers -- every window record is read ~1x instead of ~2.25x, and no thread loops
+// over a data-dependent window count.
+__global__ __launch_bounds__(256) void maxpool_bwd_s2_kernel(const bf16_t* __restrict__ dy,
+                                                             const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx,
+                                                             int N, int H, int W, int C, int P, int Q, int k,
+                                                             int pad_h, int pad_w) {
+  const int CV = C / 8;
+  const int HB = (H + 1) / 2, WB = (W + 1) / 2;
+  const int64_t total = (int64_t)N * HB * WB * CV;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % CV);
+    int64_t t = i / CV;
+    const int b = (int)(t % WB);
+    t /= WB;
+    const int a = (int)(t % HB);
+    const int n = (int)(t / HB);
+    const int h0 = 2 * a, w0 = 2 * b;
+    float acc[2][2][8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[u][v][j] = 0.f;
+    // windows p with p*2 - pad <= h <= p*2 - pad + k - 1 for h in {h0, h0 + 1}
+    // (p_lo = ceil((h0 + pad - k + 1) / 2); C's truncation only matters below 0, where max() clamps)
+    const int p_lo = max(0, (h0 + pad_h - k + 2) / 2), p_hi = min(P - 1, (h0 + 1 + pad_h) / 2);
+    const int q_lo = max(0, (w0 + pad_w - k + 2) / 2), q_hi = min(Q - 1, (w0 + 1 + pad_w) / 2);
+    for (int p = p_lo; p <= p_hi; ++p) {
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const size_t o = (((size_t)n * P + p) * Q + q) * CV + cv;
+        const uint2 ar = reinterpret_cast<const uint2*>(arg)[o];
+        float g[8];
+        unpack8(reinterpret_cast<const uint4*>(dy)[o], g);
+        const uint8_t bt[8] = {(uint8_t)(ar.x), (uint8_t)(ar.x >> 8), (uint8_t)(ar.x >> 16), (uint8_t)(ar.x >> 24),
+                               (uint8_t)(ar.y), (uint8_t)(ar.y >> 8), (uint8_t)(ar.y >> 16), (uint8_t)(ar.y >> 24)};
+        const int r0 = h0 - (2 * p - pad_h), s0 = w0 - (2 * q - pad_w);
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int v = 0; v < 2; ++v) {
+            const int r = r0 + u, s = s0 + v;
+            if (r >= 0 && r < k && s >= 0 && s < k) {
+              const int tap = r * k + s;
+#pragma unroll
+              for (int j = 0; j < 8; ++j)
+                if (bt[j] == tap) acc[u][v][j] += g[j];
+            }
+          }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+        if (h0 + u < H && w0 + v < W)
+          reinterpret_cast<uint4*>(dx)[(((size_t)n * H + h0 + u) * W + w0 + v) * CV + cv] = pack8(acc[u][v]);
+  }
+}
+
 static inline int grid_for(int64_t n) {
   int64_t b = (n + 255) / 256;
   return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
@@ -105,6 +167,12 @@ DRN_API int drn_maxpool_fwd(const void* x, void* y, uint8_t* arg, int N, int H, 
 DRN_API int drn_maxpool_bwd(const void* dy, const uint8_t* arg, void* dx, int N, int H, int W, int C, int P, int Q,
                             int k, int stride, int pad_h, int pad_w, hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
+  if (stride == 2 && k <= 4) {
+    const int64_t total = (int64_t)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+    hipLaunchKernelGGL(drn::maxpool_bwd_s2_kernel, dim3(drn::grid_for(total)), dim3(256), 0, s, (const bf16_t*)dy,
+                       arg, (bf16_t*)dx, N, H, W, C, P, Q, k, pad_h, pad_w);
+    return (int)hipGetLastError();
+  }
   const int64_t total = (int64_t)N * H * W * (C / 8);
   hipLaunchKernelGGL(drn::maxpool_bwd_kernel, dim3(drn::grid_for(total)), dim3(256), 0, s, (const bf16_t*)dy, arg,
                      (bf16_t*)dx, N, H, W, C, P, Q, k, stride, pad_h, pad_w);

@@ -24,7 +24,8 @@ class Rec(RefBackend):
         super().__init__()
         self.log = []
 
-    def conv_fwd(self, x, w, y, g, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None, bn_bwd=None):
+    def conv_fwd(self, x, w, y, g, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None, bn_bwd=None,
+                 **kw):
         K, R, S, C = w.shape
         P, Q = (out_map.P, out_map.Q) if out_map is not None else (y.shape[1], y.shape[2])
         M = x.shape[0] * P * Q

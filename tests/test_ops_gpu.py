@@ -408,10 +408,13 @@ def test_head(hip, ref):
         assert rel(a, b2) < 2e-3
 
 
-def test_maxpool(hip, ref):
+@pytest.mark.parametrize("H,pad", [(12, 0), (11, 1), (13, 0), (112, 0)])
+def test_maxpool(hip, ref, H, pad):
+    """3x3/2 max-pool forward (argmax record) and the 2x2-blocked gather backward, even and odd
+    sizes, TF 'SAME' padding (pad 0 before) and a symmetric pad."""
     torch.manual_seed(7)
-    N, H, C = 2, 12, 64
-    P = 6
+    N, C = 2, 64
+    P = (H + 2 * pad - 3) // 2 + 1 if pad else (H + 1) // 2
     x = bf(torch.randn(N, H, H, C))
     dy = bf(torch.randn(N, P, P, C))
     out = {}
@@ -419,9 +422,9 @@ def test_maxpool(hip, ref):
         xx = x.cuda() if dev == "cuda" else x.float()
         y = torch.zeros(N, P, P, C, dtype=xx.dtype, device=dev)
         arg = torch.zeros(N, P, P, C, dtype=torch.uint8, device=dev)
-        be.maxpool_fwd(xx, y, arg, 3, 2, 0, 0)
-        dx = torch.zeros_like(xx)
-        be.maxpool_bwd(dy.to(dev) if dev == "cuda" else dy.float(), arg, dx, 3, 2, 0, 0)
+        be.maxpool_fwd(xx, y, arg, 3, 2, pad, pad)
+        dx = torch.full_like(xx, 3.0)
+        be.maxpool_bwd(dy.to(dev) if dev == "cuda" else dy.float(), arg, dx, 3, 2, pad, pad)
         out[be.name] = [y.float().cpu(), arg.cpu(), dx.float().cpu()]
     assert rel(out["hip"][0], out["ref"][0]) < 1e-3
     assert rel(out["hip"][2], out["ref"][2]) < 1e-2
