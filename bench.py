@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--graph", type=int, default=-1, help="capture the step in a HIP graph (-1: auto)")
     ap.add_argument("--bucket_mb", type=float, default=25.0)
     ap.add_argument("--allreduce", default="rccl", choices=["rccl", "p2p", "auto"])
+    ap.add_argument("--shard_optimizer", type=int, default=0, help="ZeRO-1 sharded optimizer (N > 1)")
     args = ap.parse_args()
 
     import torch
@@ -83,8 +84,8 @@ def main():
     be = HipBackend("cuda")
     wd = 2e-4 if args.dataset == "cifar10" else 1e-4
     ex = Executor(spec, args.batch_size, be, "cuda", seed=1234, weight_decay=wd)
-    eng = DataParallelEngine(ex, bucket_mb=args.bucket_mb, allreduce=args.allreduce) if (world > 1 or force_dp) \
-        else None
+    eng = DataParallelEngine(ex, bucket_mb=args.bucket_mb, allreduce=args.allreduce,
+                             shard_optimizer=bool(args.shard_optimizer)) if (world > 1 or force_dp) else None
     if eng is not None:
         eng.broadcast_parameters()
     # synthetic data of the benchmark shape: fixed device batch (no host input pipeline)
@@ -99,8 +100,7 @@ def main():
             eng.begin_step()
         ex.backward()
         if eng is not None:
-            eng.finish()
-            ex.apply_gradients(grad_scale=1.0 / world)
+            eng.apply_gradients(eng.finish(), 1.0 / world)
         else:
             ex.apply_gradients()
 
@@ -113,6 +113,8 @@ def main():
     # the ~20 graph launches cost more than the host-side kernel launches they replace
     use_graph = args.graph if args.graph >= 0 else int(eng is None)
     run = step
+    if eng is not None and eng.zero1:
+        use_graph = 0
     if use_graph and eng is not None and eng.p2p is None:
         sg = SegmentedStepGraph(ex, eng, 1.0 / world, warmup=1)
         run = sg.replay

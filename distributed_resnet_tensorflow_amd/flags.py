@@ -224,6 +224,9 @@ def define_reference_flags(flag_values: FlagValues = FLAGS, **defaults) -> FlagV
     S("allreduce", "rccl", "Gradient all-reduce: rccl (RCCL ring/tree over xGMI; gloo on CPU), p2p (one-shot "
       "HIP-IPC peer kernel, one node), auto (p2p when the gradient is <= 64 MB).", fv)
     Fl("bucket_mb", 25.0, "Gradient all-reduce bucket size cap (MB of fp32).", fv)
+    B("optimizer_sharding", False, "ZeRO-1-style sharded optimizer (the parameter-server sharding analog, "
+      "SURVEY P3): reduce-scatter the gradient buckets, update 1/N of the weights and momentum per rank, "
+      "all-gather the bf16 compute weights.", fv)
     I("collective_timeout_secs", 600, "Process-group timeout and collective-watchdog limit: a rank whose "
       "gradient exchange stalls this long exits (the launcher restarts the job from its checkpoint).", fv)
     I("fault_inject_step", -1, "Kill this process at the given global step (fault-injection tests).", fv)

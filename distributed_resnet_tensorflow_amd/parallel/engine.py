@@ -21,6 +21,15 @@ ResNet-50's 102 MB of fp32 gradients -> 3 large buckets that run RCCL at link ba
 7 point-to-point xGMI links while the backward pass continues, and small final buckets, so only
 ~2 MB of all-reduce is left exposed after the backward pass.
 
+Parameter sharding over PS tasks maps to the optional ZeRO-1 mode
+(`shard_optimizer=True`, --optimizer_sharding): buckets are cut at multiples of 64 * world
+elements and REDUCE-SCATTERED instead of all-reduced, each rank runs the fused SGD-momentum on
+its 1/world slice of every bucket (so momentum updates and optimizer HBM traffic are sharded),
+then the bf16 compute weights are ALL-GATHERED (half the bytes of fp32): per step 0.75x the
+collective bytes of the all-reduce path, with the weight gather exposed after the backward pass.
+Masters / momentum outside a rank's shard go stale and are all-gathered by `gather_state()`
+before a checkpoint is written (a collective: every rank takes part in the save decision).
+
 Async PS training (--sync_replicas=False with --job_name set) maps to
 `mode="delayed"`: step t applies the averaged gradient of step t-1 while step t's all-reduce
 runs behind step t+1's compute (bounded staleness 1, no PS).
@@ -39,7 +48,7 @@ from .watchdog import CollectiveWatchdog
 class DataParallelEngine:
     def __init__(self, executor, bucket_mb: float = 25.0, mode: str = "sync", group=None,
                  allreduce: str = "rccl", p2p_max_mb: float = 64.0, first_bucket_mb: float = 2.0,
-                 timeout_s: float = 0.0):
+                 timeout_s: float = 0.0, shard_optimizer: bool = False):
         self.ex = executor
         self.P = executor.P
         self.group = group
@@ -58,6 +67,11 @@ class DataParallelEngine:
             if len(self.buckets) + 1 >= 64:
                 self.buckets = self._make_buckets(int(self.P.total // 60) + 1)
             self.p2p = P2PAllReduce(self.P.grad, group)
+        self.zero1 = bool(shard_optimizer) and self.world > 1 and mode == "sync"
+        if self.zero1:
+            if self.p2p is not None:
+                raise ValueError("optimizer sharding uses reduce-scatter / all-gather collectives, not --allreduce=p2p")
+            self.buckets = self._align_buckets(self.buckets, 64 * self.world)
         self.works: List = []
         self.launched = [False] * len(self.buckets)
         self.frontier = self.P.total
@@ -91,6 +105,28 @@ class DataParallelEngine:
             buckets.append((lo, self.P.total))
         return buckets[::-1]
 
+    def _align_buckets(self, buckets, align: int):
+        """Bucket boundaries rounded down to multiples of `align` (= 64 * world), so every bucket
+        but the one ending at the buffer's end splits into `world` equal 256-byte-aligned shards.
+        A bucket is still launched only once its whole range is complete (lo >= frontier)."""
+        bounds = sorted({(lo // align) * align for lo, _ in buckets} | {0})
+        out, prev = [], None
+        for b in bounds + [self.P.total]:
+            if prev is not None and b > prev:
+                out.append((prev, b))
+            prev = b
+        return out[::-1]
+
+    def _sharded(self, lo: int, hi: int) -> bool:
+        return self.zero1 and (hi - lo) % self.world == 0
+
+    def _shard(self, lo: int, hi: int):
+        """This rank's slice of bucket [lo, hi) (the whole bucket when it is not sharded)."""
+        if not self._sharded(lo, hi):
+            return lo, hi
+        c = (hi - lo) // self.world
+        return lo + self.rank * c, lo + (self.rank + 1) * c
+
     # -- hooks --------------------------------------------------------------------------------------
     def begin_step(self):
         self.works = []
@@ -120,7 +156,14 @@ class DataParallelEngine:
             self.launched[i] = True
             return
         t = (self.P.grad if buf is None else buf)[lo:hi]
-        self.works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        if self._sharded(lo, hi):
+            # in place: this rank's shard of the bucket receives the sum over ranks
+            s0, s1 = self._shard(lo, hi)
+            out = (self.P.grad if buf is None else buf)[s0:s1]
+            self.works.append(dist.reduce_scatter_tensor(out, t, op=dist.ReduceOp.SUM, group=self.group,
+                                                         async_op=True))
+        else:
+            self.works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
         self.launched[i] = True
 
     def _on_ready(self, lo_ready: int):
@@ -173,6 +216,44 @@ class DataParallelEngine:
             self._launch(i, self.comm_grad)
         self._delayed_pending = True
         return self.ready_grad
+
+    def apply_gradients(self, grad: torch.Tensor, grad_scale: float):
+        """The optimizer step after finish(): the executor's fused update (plain data parallel), or
+        -- ZeRO-1 -- the update of this rank's shards followed by the all-gather of the compute
+        weights and the refresh of the data-gradient weights."""
+        if not self.zero1:
+            self.ex.apply_gradients(grad_scale=grad_scale, grad=grad)
+            return
+        for lo, hi in self.buckets:
+            s0, s1 = self._shard(lo, hi)
+            self.ex.sgd_range(s0, s1, grad_scale, grad=grad)
+        src = self.P.wbf16 if self.P.wbf16 is not None else self.P.master
+        works = []
+        for lo, hi in self.buckets:
+            if self._sharded(lo, hi):
+                s0, s1 = self._shard(lo, hi)
+                works.append(dist.all_gather_into_tensor(src[lo:hi], src[s0:s1], group=self.group, async_op=True))
+        for w in works:
+            w.wait()
+        self.ex.refresh_dgrad_weights()
+
+    def gather_state(self):
+        """ZeRO-1: make the fp32 masters and momentum complete on every rank (collective; before a
+        checkpoint or anything else that reads them). No-op otherwise."""
+        if not self.zero1:
+            return
+        for t in (self.P.master, self.P.momentum):
+            for lo, hi in self.buckets:
+                if self._sharded(lo, hi):
+                    s0, s1 = self._shard(lo, hi)
+                    dist.all_gather_into_tensor(t[lo:hi], t[s0:s1], group=self.group)
+
+    def agree(self, flag: bool) -> bool:
+        """Rank 0's decision, on every rank (collective)."""
+        dev = self.P.master.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+        t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+        dist.broadcast(t, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0, group=self.group)
+        return bool(t.item())
 
     def stats(self) -> dict:
         """Timing of the last completed step (synchronizes on its events)."""

@@ -690,6 +690,19 @@ class Executor:
         P = self.P
         g = P.grad if grad is None else grad
         self.be.sgd_momentum(P.master, P.momentum, g, P.wbf16, self.lr_t, self.mom, self.wd, grad_scale)
+        self.refresh_dgrad_weights()
+
+    def sgd_range(self, lo: int, hi: int, grad_scale: float, grad: Optional[torch.Tensor] = None):
+        """Fused SGD-momentum on the flat slice [lo, hi) only (sharded optimizer)."""
+        P = self.P
+        g = P.grad if grad is None else grad
+        wb = P.wbf16[lo:hi] if P.wbf16 is not None else None
+        self.be.sgd_momentum(P.master[lo:hi], P.momentum[lo:hi], g[lo:hi], wb, self.lr_t, self.mom, self.wd,
+                             grad_scale)
+
+    def refresh_dgrad_weights(self):
+        """Rebuild the flipped / channel-transposed data-gradient weights from the compute copy."""
+        P = self.P
         if self.wt_n:
             src = P.wbf16 if P.wbf16 is not None else P.master
             table = self.wt_table if self.is_hip else self.wt_table.cpu()

@@ -95,9 +95,14 @@ class SummaryHook(Hook):
 
 
 class CheckpointHook(Hook):
-    def __init__(self, save_secs: float, save_fn):
+    """Time-based checkpoints (MonitoredTrainingSession save_checkpoint_secs) + one at the end.
+    `agree` (sharded optimizer: the hook runs on every rank and the save is collective) turns the
+    chief's timer decision into every rank's decision."""
+
+    def __init__(self, save_secs: float, save_fn, agree=None):
         self.secs = save_secs
         self.save_fn = save_fn
+        self.agree = agree
         self._last = None
         self._last_step = -1
 
@@ -105,7 +110,10 @@ class CheckpointHook(Hook):
         self._last = time.time()
 
     def after_step(self, sess, step, metrics_fn):
-        if self.secs > 0 and time.time() - self._last >= self.secs:
+        due = self.secs > 0 and time.time() - self._last >= self.secs
+        if self.agree is not None:
+            due = self.agree(due)
+        if due:
             self.save_fn(step, blocking=False)
             self._last = time.time()
             self._last_step = step

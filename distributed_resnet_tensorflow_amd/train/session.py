@@ -46,7 +46,7 @@ class TrainingSession:
     def __init__(self, spec, batch: int, cluster, *, weight_decay: float, lr_schedule, checkpoint_dir: str = "",
                  max_to_keep: int = 5, seed: int = 0, use_graph: bool = True, sync_mode: str = "sync",
                  bucket_mb: float = 25.0, meta: Optional[dict] = None, allreduce: str = "rccl",
-                 collective_timeout_s: float = 0.0, precision: str = "bf16"):
+                 collective_timeout_s: float = 0.0, precision: str = "bf16", shard_optimizer: bool = False):
         self.cluster = cluster
         self.spec = spec
         self.device = torch.device(cluster.device)
@@ -55,7 +55,9 @@ class TrainingSession:
         self.lr = lr_schedule
         self.meta = meta or {}
         self.engine = DataParallelEngine(self.ex, bucket_mb=bucket_mb, mode=sync_mode, allreduce=allreduce,
-                                         timeout_s=collective_timeout_s) if cluster.distributed else None
+                                         timeout_s=collective_timeout_s,
+                                         shard_optimizer=shard_optimizer) if cluster.distributed else None
+        self.sharded = self.engine is not None and self.engine.zero1
         self.world = cluster.world
         self.ckpt_dir = checkpoint_dir
         self.saver = Saver(checkpoint_dir, max_to_keep) if (checkpoint_dir and cluster.is_chief) else None
@@ -74,7 +76,7 @@ class TrainingSession:
         # chain of per-segment graphs, SegmentedStepGraph, which DRN_DP_GRAPH=1 selects)
         self.use_graph = use_graph and self.device.type == "cuda" and self.be.name == "hip" and (
             not cluster.distributed or (os.environ.get("DRN_DP_GRAPH") == "1" and self.engine.p2p is None
-                                        and self.engine.mode == "sync"))
+                                        and self.engine.mode == "sync" and not self.sharded))
         self._graph: Optional[StepGraph] = None
         self._metrics_cache = None
         self.cur_lr = float("nan")
@@ -97,6 +99,10 @@ class TrainingSession:
                 self.data_state = {}
 
     def save(self, step: Optional[int] = None, blocking: bool = True):
+        """Chief writes the checkpoint. With the sharded optimizer every rank must call this (the
+        masters / momentum are first all-gathered)."""
+        if self.sharded:
+            self.engine.gather_state()
         if self.saver is None:
             return None
         step = self.global_step if step is None else step
@@ -114,7 +120,7 @@ class TrainingSession:
             self.engine.begin_step()
             ex.backward()
             g = self.engine.finish()
-            ex.apply_gradients(grad_scale=1.0 / self.world, grad=g)
+            self.engine.apply_gradients(g, 1.0 / self.world)
         else:
             ex.backward()
             ex.apply_gradients()

@@ -98,7 +98,8 @@ def train(FLAGS, cluster=None):
                            checkpoint_dir=FLAGS.log_root, max_to_keep=FLAGS.max_to_keep, seed=FLAGS.seed,
                            use_graph=FLAGS.hip_graph, sync_mode=sync_mode, bucket_mb=FLAGS.bucket_mb,
                            meta=_meta(FLAGS, spec), allreduce=FLAGS.allreduce,
-                           collective_timeout_s=FLAGS.collective_timeout_secs, precision=FLAGS.precision)
+                           collective_timeout_s=FLAGS.collective_timeout_secs, precision=FLAGS.precision,
+                           shard_optimizer=FLAGS.optimizer_sharding)
     feeder = make_feeder(FLAGS, sess.ex, cluster, True, sess.data_state)
     is_imagenet = FLAGS.dataset == "imagenet"
     hooks = [LoggingHook(FLAGS.log_every_n_steps, FLAGS.batch_size * cluster.world,
@@ -112,7 +113,11 @@ def train(FLAGS, cluster=None):
     if summary_dir and FLAGS.save_summaries_steps > 0:
         chief_hooks.append(SummaryHook(EventFileWriter(summary_dir), FLAGS.save_summaries_steps))
     if FLAGS.log_root:
-        chief_hooks.append(CheckpointHook(FLAGS.save_checkpoint_secs, lambda step, blocking: sess.save(step, blocking)))
+        save_fn = lambda step, blocking: sess.save(step, blocking)  # noqa: E731
+        if sess.sharded:  # collective save: every rank gathers its optimizer shards
+            hooks.append(CheckpointHook(FLAGS.save_checkpoint_secs, save_fn, agree=sess.engine.agree))
+        else:
+            chief_hooks.append(CheckpointHook(FLAGS.save_checkpoint_secs, save_fn))
     if FLAGS.profile_steps:
         chief_hooks.append(ProfileHook(FLAGS.profile_steps, FLAGS.log_root or "."))
     try:

@@ -57,8 +57,10 @@ def test_ps_task_exits_cleanly(tmp_path):
     assert r.returncode == 0 and "parameter servers are not used" in r.stdout
 
 
-def test_two_worker_fake_cluster(cifar_dir, tmp_path):
-    """--job_name=worker --task_index=i over localhost ports (reference submit_mac_dist.sh)."""
+@pytest.mark.parametrize("shard", [False, True])
+def test_two_worker_fake_cluster(cifar_dir, tmp_path, shard):
+    """--job_name=worker --task_index=i over localhost ports (reference submit_mac_dist.sh); shard:
+    the ZeRO-1 optimizer (--optimizer_sharding), whose checkpoint save is collective."""
     import socket
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -68,6 +70,8 @@ def test_two_worker_fake_cluster(cifar_dir, tmp_path):
     base = ["resnet_cifar_main.py", "--job_name=worker", f"--worker_hosts=127.0.0.1:{port},127.0.0.1:{port + 1}",
             "--ps_hosts=127.0.0.1:2230", "--sync_replicas=True", f"--train_data_path={cifar_dir}", f"--log_root={ck}",
             "--resnet_size=8", "--batch_size=8", "--train_steps=6", "--log_every_n_steps=3"]
+    if shard:
+        base += ["--optimizer_sharding=True", "--save_checkpoint_secs=1"]
     e = dict(os.environ, PYTHONPATH=REPO)
     ps = [subprocess.Popen([PY] + base + [f"--task_index={i}"], cwd=REPO, env=e, stdout=subprocess.PIPE,
                            stderr=subprocess.STDOUT, text=True) for i in range(2)]

@@ -152,3 +152,55 @@ def test_collective_watchdog_fires_on_stalled_exchange():
     time.sleep(0.4)
     assert not wd.fired and len(msgs) == n
     wd.close()
+
+
+def _zero1_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2
+        from distributed_resnet_tensorflow_amd.parallel.engine import DataParallelEngine
+        spec = cifar_resnet_v2(8)
+        out = {}
+        for shard in (False, True):
+            ex = _grads_for(spec, 4, rank, seed=1)
+            eng = DataParallelEngine(ex, bucket_mb=0.05, shard_optimizer=shard)
+            assert eng.zero1 == shard
+            if shard:  # every bucket but the one at the buffer end splits into equal shards
+                assert sum(eng._sharded(lo, hi) for lo, hi in eng.buckets) >= len(eng.buckets) - 1
+                assert eng.buckets[0][1] == ex.P.total and eng.buckets[-1][0] == 0
+            eng.broadcast_parameters()
+            ex.set_lr(0.1)
+            for _ in range(2):
+                ex.forward(True)
+                eng.begin_step()
+                ex.backward()
+                eng.apply_gradients(eng.finish(), 1.0 / world)
+            eng.gather_state()
+            out[shard] = (ex.P.master.clone(), ex.P.momentum.clone())
+        rel = lambda a, b: ((a - b).norm() / b.norm()).item()  # noqa: E731
+        q.put((rank, rel(out[True][0], out[False][0]), rel(out[True][1], out[False][1])))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), None))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_optimizer_matches_allreduce_dp(world):
+    """ZeRO-1 (reduce-scatter, per-rank SGD shard, all-gather of the weights) trains to the same
+    weights and momentum as all-reduce data parallelism over two steps (the second step uses
+    weights the first step's gather produced; gather_state completes the stale shards)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_zero1_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, ew, em in res:
+        assert isinstance(ew, float), ew
+        assert ew < 1e-6 and em < 1e-5, (rank, ew, em)
