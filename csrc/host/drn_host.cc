@@ -15,22 +15,21 @@
 #define DRN_HOST_API extern "C" __attribute__((visibility("default")))
 
 namespace {
-uint32_t g_table[256];
-bool g_table_init = false;
-
-void init_table() {
-  for (uint32_t i = 0; i < 256; ++i) {
-    uint32_t c = i;
-    for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : (c >> 1);
-    g_table[i] = c;
+struct CrcTable {
+  uint32_t t[256];
+  CrcTable() {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x82F63B78u : (c >> 1);
+      t[i] = c;
+    }
   }
-  g_table_init = true;
-}
+};
 
 uint32_t crc_sw(const uint8_t* p, size_t n, uint32_t crc) {
-  if (!g_table_init) init_table();
+  static const CrcTable table;  // thread-safe one-time initialisation (reader threads call this)
   crc = ~crc;
-  for (size_t i = 0; i < n; ++i) crc = g_table[(crc ^ p[i]) & 0xff] ^ (crc >> 8);
+  for (size_t i = 0; i < n; ++i) crc = table.t[(crc ^ p[i]) & 0xff] ^ (crc >> 8);
   return ~crc;
 }
 
@@ -59,6 +58,9 @@ DRN_HOST_API uint32_t drn_crc32c(const uint8_t* data, size_t n, uint32_t init) {
   return crc_sw(data, n, init);
 }
 
+// Table-driven path regardless of the CPU (tests compare it against the SSE4.2 path).
+DRN_HOST_API uint32_t drn_crc32c_sw(const uint8_t* data, size_t n, uint32_t init) { return crc_sw(data, n, init); }
+
 DRN_HOST_API uint32_t drn_crc32c_masked(const uint8_t* data, size_t n) {
   const uint32_t c = drn_crc32c(data, n, 0);
   return ((c >> 15) | (c << 17)) + 0xa282ead8u;
@@ -78,7 +80,7 @@ DRN_HOST_API long drn_tfrecord_scan(const uint8_t* buf, size_t n, int64_t* offse
       std::memcpy(&lcrc, buf + pos + 8, 4);
       if (drn_crc32c_masked(buf + pos, 8) != lcrc) return -(cnt + 1);
     }
-    if (pos + 12 + len + 4 > n) return -(cnt + 1);
+    if (len > n - pos - 12 || n - pos - 12 - len < 4) return -(cnt + 1);  // no wrap-around on a corrupt length
     if (check) {
       uint32_t dcrc;
       std::memcpy(&dcrc, buf + pos + 12 + len, 4);

@@ -19,6 +19,7 @@ import shutil
 import subprocess
 import sys
 from pathlib import Path
+from typing import Optional
 
 REPO = Path(__file__).resolve().parents[2]
 CSRC = REPO / "csrc"
@@ -58,6 +59,25 @@ def _compile(src: Path, extra: list[str]) -> Path:
     if res.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{res.stderr[-6000:]}")
     return obj
+
+
+def build_host_sanitizer_driver(kind: str = "address", out_dir: Optional[str] = None) -> Path:
+    """Build csrc/host/tests/host_sanitize_main.cc + the host helpers as an executable under a
+    host-code sanitizer: kind "address" = ASan + UBSan, "thread" = TSan. GPU
+    sanitizers are not available on the MI355X pool; the kernels are covered by the DRN_CHECK_NAN
+    and DRN_DETERMINISTIC modes instead."""
+    import tempfile
+    cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
+    san = {"address": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
+           "thread": ["-fsanitize=thread"]}[kind]
+    out = Path(out_dir or tempfile.mkdtemp(prefix="drn_san_")) / f"host_sanitize_{kind}"
+    srcs = sorted(HOST_SRC.glob("*.cc")) + [HOST_SRC / "tests" / "host_sanitize_main.cc"]
+    cmd = [cxx, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-pthread"] + san + \
+        ["-o", str(out)] + [str(s) for s in srcs]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"sanitizer driver build failed:\n{res.stderr[-4000:]}")
+    return out
 
 
 def build_host(force: bool = False, verbose: bool = True) -> Path:
