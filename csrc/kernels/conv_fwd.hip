@@ -511,9 +511,17 @@ __device__ __forceinline__ int glds_swz(int row) {
 // barrier and no extra HBM pass; pieces read from the zero page (padding, rows past M) are
 // skipped and stay zero. The per-channel scale/shift are staged once into LDS behind the
 // pipeline stages. Used for 1x1 consumers, where it replaces a full streaming BN-apply pass.
-template <int BP, int BC, int WAVES_P, int NS, int NW = 4, bool PF = true, int BK = 64, bool PRO = false>
+//
+// SROW: narrow-input convolutions (C == 8: the ImageNet 7x7/2 stem on RGB padded to 8 channels)
+// stage ONE FILTER ROW r per step: the 8 16-byte chunks of a 64-deep stage are the taps
+// s = 0..7 of that row (8 channels each; tap S..7 are zero-page pieces on both operands), so
+// k = (r, s, c) keeps the reduction on the LDS-DMA path (per-lane pixel / tap validity) at
+// 8/7 of the 7x7x8 work instead of falling back to the register-staged kernel.
+template <int BP, int BC, int WAVES_P, int NS, int NW = 4, bool PF = true, int BK = 64, bool PRO = false,
+          bool SROW = false>
 __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a, const void* __restrict__ zero) {
   static_assert(BK == 64 || BK == 32, "k per stage");
+  static_assert(!SROW || (BK == 64 && !PRO), "row-staged narrow convs: 64-deep stages, no fused prologue");
   constexpr int NT = NW * 64;
   constexpr int WAVES_C = NW / WAVES_P;
   constexpr int WP = BP / WAVES_P, WC = BC / WAVES_C;
@@ -549,18 +557,21 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   const int lpc = lane % CPR;
   const bf16_t* __restrict__ xg = reinterpret_cast<const bf16_t*>(a.x);
   const bf16_t* wsrc[GA];
+  int alc[GA];  // SROW: the lane's logical chunk = filter tap s of its weight rows
 #pragma unroll
   for (int i = 0; i < GA; ++i) {
     const int row = RPG * NW * i + RPG * wave + lrow;
     const int lc = lpc ^ glds_swz<BK>(row);
     const int c = c0 + row;
-    wsrc[i] = c < a.K ? reinterpret_cast<const bf16_t*>(a.w) + (size_t)c * Ktot + lc * 8 : nullptr;
+    alc[i] = lc;
+    wsrc[i] = c < a.K ? reinterpret_cast<const bf16_t*>(a.w) + (size_t)c * Ktot + (SROW ? 0 : lc * 8) : nullptr;
   }
-  int boff[GB], bh[GB], bw[GB];
+  int boff[GB], bh[GB], bw[GB], blc[GB];
 #pragma unroll
   for (int i = 0; i < GB; ++i) {
     const int row = RPG * NW * i + RPG * wave + lrow;
     const int lc = lpc ^ glds_swz<BK>(row);  // (BC + row) has the same swizzle bits
+    blc[i] = lc;
     const int m = m0 + row;
     if (m < M) {
       const int pq = a.P * a.Q;
@@ -570,7 +581,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
       const int q = rem - p * a.Q;
       bh[i] = p * a.stride - a.pad_h;
       bw[i] = q * a.stride - a.pad_w;
-      boff[i] = ((n * a.H + bh[i]) * a.W + bw[i]) * C + lc * 8;
+      boff[i] = ((n * a.H + bh[i]) * a.W + bw[i]) * C + (SROW ? 0 : lc * 8);
     } else {
       bh[i] = -(1 << 28);
       bw[i] = 0;
@@ -582,6 +593,22 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
 
   auto issue = [&](int slot) {
     char* st = smem + slot * STAGE;
+    if constexpr (SROW) {  // stage = filter row ir; chunk lc = tap s
+#pragma unroll
+      for (int i = 0; i < GA; ++i) {
+        const void* src = (wsrc[i] && alc[i] < a.S) ? (const void*)(wsrc[i] + (ir * a.S + alc[i]) * 8) : zero;
+        glds16(src, st + (RPG * NW * i + RPG * wave) * ROWB);
+      }
+#pragma unroll
+      for (int i = 0; i < GB; ++i) {
+        const int h = bh[i] + ir, w = bw[i] + blc[i];
+        const bool ok = blc[i] < a.S && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+        const void* src = ok ? (const void*)(xg + (boff[i] + (ir * a.W + blc[i]) * 8)) : zero;
+        glds16(src, st + (BC + RPG * NW * i + RPG * wave) * ROWB);
+      }
+      ++ir;
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
       const void* src = wsrc[i] ? (const void*)(wsrc[i] + ik) : zero;
@@ -623,7 +650,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   for (int j = 0; j < MJ; ++j) boffl[j] = (BC + wp * WP + j * 16 + fr) * ROWB;
   const int swz = glds_swz<BK>(fr);  // fragment row groups are 16-aligned: the swizzle bits are fr's
 
-  const int T = Ktot / BK;
+  const int T = SROW ? a.R : Ktot / BK;
   // fused-BN operands: [scale C][shift C] fp32 behind the stages (before any LDS-DMA is issued)
   float* const ssl = reinterpret_cast<float*>(smem + NS * STAGE);
   if constexpr (PRO) {
@@ -709,14 +736,14 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   conv_epilogue<BP, BC, WP, WC, MI, MJ, NT, PF>(a, smem, acc, wp, wc, m0, c0, M, epre);
 }
 
-template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF, int BK, bool PRO>
+template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF, int BK, bool PRO, bool SROW = false>
 static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
   constexpr int LDS0 = NS * (BC + BP) * BK * 2;
   const int lds_main = LDS0 + (PRO ? 8 * a->C : 0);                 // + fused-BN scale/shift
   const int LDS = lds_main > BP * BC * 4 ? lds_main : BP * BC * 4;  // epilogue staging tile
   if (LDS > 160 * 1024) return (int)hipErrorInvalidValue;
   static bool attr_set = false;
-  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS, NW, PF, BK, PRO>;
+  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS, NW, PF, BK, PRO, SROW>;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
@@ -732,8 +759,16 @@ static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t 
 // epilogue operands (residual / BN-backward input) are prefetched only when present
 template <int BP, int BC, int WAVES_P, int NS, int NW = 4, int BK = 64>
 static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
-  if (a->C % BK) return (int)hipErrorInvalidValue;
   const bool pf = a->residual != nullptr || a->bn_x != nullptr;
+  if (a->C == 8) {  // row-staged narrow conv (the stem)
+    if constexpr (BK == 64) {
+      if (a->S > 8 || a->in_scale != nullptr) return (int)hipErrorInvalidValue;
+      return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, false, true>(a, zero, stream)
+                : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false, true>(a, zero, stream);
+    }
+    return (int)hipErrorInvalidValue;
+  }
+  if (a->C % BK) return (int)hipErrorInvalidValue;
   if (a->in_scale != nullptr)
     return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, true>(a, zero, stream)
               : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, true>(a, zero, stream);
@@ -797,6 +832,7 @@ static int glds_cfg_bp(int cfg) {
 // 64 x 128 tiles once the 128 x 128 grid stops filling the chip.
 static int glds_default_cfg(const DrnConvFwdArgs* a) {
   const long M = (long)a->N * a->P * a->Q;
+  if (a->C == 8) return a->K <= 64 ? 3 : 0;  // row-staged narrow conv: 64-deep stages only
   if (a->C % 64) return 18;  // 32-channel inputs: the 32-deep-stage family
   auto blocks = [&](int bp, int bc) { return ((M + bp - 1) / bp) * ((a->K + bc - 1) / bc); };
   if (a->K <= 64) return blocks(256, 64) >= 384 ? 3 : 7;
@@ -842,6 +878,8 @@ DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s);
 
 // Whether the LDS-DMA kernel family supports this convolution.
 DRN_API int drn_conv_glds_ok(const DrnConvFwdArgs* a) {
+  if (a->C == 8)  // row-staged narrow conv (stem): no fused BN prologue
+    return a->dil == 1 && a->S <= 8 && a->in_scale == nullptr;
   return a->C % 32 == 0 && a->dil == 1 && (a->in_scale == nullptr || (a->C <= 4096 && a->relu_in != 0));
 }
 
