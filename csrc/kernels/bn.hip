@@ -48,11 +48,11 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict_
       }
     }
   }
-  float* red = reinterpret_cast<float*>(smem);  // [256][16]
+  float* red = reinterpret_cast<float*>(smem);  // [256][17] (padded row: no bank conflicts)
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    red[tid * 16 + j] = s[j];
-    red[tid * 16 + 8 + j] = q[j];
+    red[tid * 17 + j] = s[j];
+    red[tid * 17 + 8 + j] = q[j];
   }
   __syncthreads();
   // thread t < C*2 produces channel c = t>>1, which = t&1
@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const bf16_t* __restrict_
     const int c = t >> 1, which = t & 1;
     const int cvv = c / 8, j = c % 8;
     float acc = 0.f;
-    for (int r = 0; r < rpp; ++r) acc += red[(r * CV + cvv) * 16 + which * 8 + j];
+    for (int r = 0; r < rpp; ++r) acc += red[(r * CV + cvv) * 17 + which * 8 + j];
     atomicAdd(part + ((size_t)(blockIdx.x % rep) * 2 + which) * C + c, acc);
   }
 }
@@ -305,15 +305,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(DySrc src, const bf1
   float* red = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    red[tid * 16 + j] = sg[j];
-    red[tid * 16 + 8 + j] = sgx[j];
+    red[tid * 17 + j] = sg[j];
+    red[tid * 17 + 8 + j] = sgx[j];
   }
   __syncthreads();
   for (int t = tid; t < 2 * C; t += 256) {
     const int ch = t >> 1, which = t & 1;
     const int cvv = ch / 8, j = ch % 8;
     float acc = 0.f;
-    for (int r = 0; r < rpp; ++r) acc += red[(r * CV + cvv) * 16 + which * 8 + j];
+    for (int r = 0; r < rpp; ++r) acc += red[(r * CV + cvv) * 17 + which * 8 + j];
     atomicAdd(part + ((size_t)(blockIdx.x % rep) * 2 + which) * C + ch, acc);
   }
 }
@@ -453,7 +453,7 @@ DRN_API int drn_bn_stats_blocks(int M, int C, int rows_per_block) { return (M + 
 DRN_API int drn_bn_stats(const void* x, float* part, int M, int C, int rows_per_block, int rep, hipStream_t s) {
   if (C % 8 || C / 8 > 256 || rep < 1) return (int)hipErrorInvalidValue;
   const int G = (M + rows_per_block - 1) / rows_per_block;
-  hipLaunchKernelGGL(drn::bn_stats_kernel, dim3(G), dim3(256), 256 * 16 * 4, s, (const bf16_t*)x, part, M, C,
+  hipLaunchKernelGGL(drn::bn_stats_kernel, dim3(G), dim3(256), 256 * 17 * 4, s, (const bf16_t*)x, part, M, C,
                      rows_per_block, rep);
   return (int)hipGetLastError();
 }
@@ -514,7 +514,7 @@ DRN_API int drn_bn_bwd_reduce(const void* dy, const float* dpool, int pool_hw, c
   if (C % 8 || C / 8 > 256 || rep < 1) return (int)hipErrorInvalidValue;
   const int G = (M + rows_per_block - 1) / rows_per_block;
   drn::DySrc src{(const bf16_t*)dy, dpool, pool_hw};
-  hipLaunchKernelGGL(drn::bn_bwd_reduce_kernel, dim3(G), dim3(256), 256 * 16 * 4, s, src, (const bf16_t*)x, scale,
+  hipLaunchKernelGGL(drn::bn_bwd_reduce_kernel, dim3(G), dim3(256), 256 * 17 * 4, s, src, (const bf16_t*)x, scale,
                      shift, mean, invstd, part, M, C, rows_per_block, relu, rep);
   return (int)hipGetLastError();
 }

@@ -241,18 +241,19 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
   }
   if (want_stats) {
     __syncthreads();
-    float* red = tile;  // [NT][16]
+    float* red = tile;  // [NT][17]: row stride 17 floats keeps the per-j column writes and the
+                        // strided reads bank-conflict free (stride 16 was a 16-way conflict)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      red[tid * 16 + j] = ssum[j];
-      red[tid * 16 + 8 + j] = ssq[j];
+      red[tid * 17 + j] = ssum[j];
+      red[tid * 17 + 8 + j] = ssq[j];
     }
     __syncthreads();
     for (int t = tid; t < 2 * BC; t += NT) {  // 2*BC may exceed the thread count (BC = 256)
       const int cl = t >> 1, which = t & 1;
       const int chh = cl >> 3, j = cl & 7;
       float s = 0.f;
-      for (int t2 = chh; t2 < NT; t2 += CHR) s += red[t2 * 16 + which * 8 + j];
+      for (int t2 = chh; t2 < NT; t2 += CHR) s += red[t2 * 17 + which * 8 + j];
       const int rep = a.stats_rep > 1 ? a.stats_rep : 1;
       if (c0 + cl < a.K) atomicAdd(a.stats + ((size_t)(blockIdx.x % rep) * 2 + which) * a.K + c0 + cl, s);
     }
