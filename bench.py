@@ -68,6 +68,11 @@ def main():
     if force_dp and world == 1 and "MASTER_ADDR" not in os.environ:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("DRN_BENCH_PORT", "29533"),
                           RANK="0", WORLD_SIZE="1")
+    if (world > 1 or force_dp) and args.graph != 1:
+        # eager data-parallel step: its main (critical-path) stream at HIGH priority -- see
+        # parallel.engine.use_priority_main_stream
+        from distributed_resnet_tensorflow_amd.parallel.engine import use_priority_main_stream
+        use_priority_main_stream()
     if world > 1 or force_dp:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))

@@ -45,6 +45,24 @@ import torch.distributed as dist
 from .watchdog import CollectiveWatchdog
 
 
+def use_priority_main_stream():
+    """Run this thread's subsequent GPU work (the eager data-parallel step) on a HIGH-priority
+    stream. HIP serves each priority level from its own hardware queues; with the default 4 HW
+    queues per process, once RCCL's streams exist a normal-priority main stream was measured
+    sharing one in-order queue with the executor's weight-gradient side stream -- no
+    wgrad/dgrad overlap (one-GPU single-rank engine: 12.9-13.0 ms vs 11.3 ms per ResNet-50 step).
+    Not for HIP-graph capture: a graph replayed from a high-priority stream measured 19.4 vs
+    11.2 ms. DRN_MAIN_PRIORITY=0 disables it. Returns the stream (None when disabled)."""
+    import os
+    prio = int(os.environ.get("DRN_MAIN_PRIORITY", "-1"))
+    if prio == 0 or not torch.cuda.is_available():
+        return None
+    s = torch.cuda.Stream(priority=prio)
+    s.wait_stream(torch.cuda.current_stream())
+    torch.cuda.set_stream(s)
+    return s
+
+
 class DataParallelEngine:
     def __init__(self, executor, bucket_mb: float = 25.0, mode: str = "sync", group=None,
                  allreduce: str = "rccl", p2p_max_mb: float = 64.0, first_bucket_mb: float = 2.0,

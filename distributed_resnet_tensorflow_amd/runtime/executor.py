@@ -549,25 +549,15 @@ class Executor:
         hw = self.last_out.shape[1] * self.last_out.shape[2]
         d_out = self._view(self.g_a, self.last_out)
         self._bn_bwd(fb, self.last_out, None, d_out, dpool=self.dpool, pool_hw=hw)
-        if self.grad_ready is not None:
-            self.grad_ready(self.P.by_name[f"{fb.bn.name}/gamma"].offset)
+        self._report(self.P.by_name[f"{fb.bn.name}/gamma"].offset)
         bufs = [self.g_a, self.g_b, self.g_c]
         cur = 0  # index of the buffer holding d_out
         self._pending.clear()
-        lagged = None  # (lo, side event) of the previous block: reported one block late, so the
-        #               main stream waits on weight gradients that have (almost surely) finished
         for bp in reversed(self.blocks):
             cur = self._block_bwd(bp, bufs, cur)
             if self.check_nan:
                 self._check(self._view(bufs[cur], bp.x), f"input gradient of block {bp.blk.stage}.{bp.blk.index}")
-            if self.grad_ready is not None:
-                if self.side is None:
-                    self.grad_ready(bp.grad_lo)
-                else:
-                    if lagged is not None:
-                        self._join(lagged[1])
-                        self.grad_ready(lagged[0])
-                    lagged = (bp.grad_lo, self._side_mark())
+            self._report(bp.grad_lo)
         d_x0 = self._view(bufs[cur], self.blocks[0].x)
         st = self.stem_op
         if sp.maxpool:
@@ -579,11 +569,22 @@ class Executor:
         else:
             d_stem = d_x0
         self._wgrad(self.images, d_stem, st.dw, st.geom)
+        self._report(0)
         self._join()
-        if self.grad_ready is not None:
-            if lagged is not None:
-                self.grad_ready(lagged[0])
-            self.grad_ready(0)
+
+    def _report(self, lo: int):
+        """grad_ready(lo): every gradient at flat offsets >= lo is issued. With the weight-gradient
+        side stream the report is made FROM that stream after it has caught up with the main
+        stream, so the bucket collectives it launches are ordered after both streams' producers
+        while the main stream's data-gradient chain never waits for the side stream."""
+        if self.grad_ready is None:
+            return
+        if self.side is None:
+            self.grad_ready(lo)
+            return
+        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.side):
+            self.grad_ready(lo)
 
     # -- weight gradients on the side stream ---------------------------------------------------------
     def _wgrad(self, x, dy, dw, geom, in_bn=None, dy_buf=None):
@@ -605,14 +606,6 @@ class Executor:
         ev = self._pending.pop(id(buf), None)
         if ev is not None:
             torch.cuda.current_stream(self.device).wait_event(ev)
-
-    def _side_mark(self):
-        """Event after every weight gradient issued so far (None without a side stream)."""
-        if self.side is None:
-            return None
-        ev = torch.cuda.Event()
-        ev.record(self.side)
-        return ev
 
     def _join(self, ev=None):
         if self.side is None:

@@ -77,6 +77,9 @@ class TrainingSession:
         self.use_graph = use_graph and self.device.type == "cuda" and self.be.name == "hip" and (
             not cluster.distributed or (os.environ.get("DRN_DP_GRAPH") == "1" and self.engine.p2p is None
                                         and self.engine.mode == "sync" and not self.sharded))
+        if cluster.distributed and not self.use_graph and self.device.type == "cuda":
+            from ..parallel.engine import use_priority_main_stream
+            use_priority_main_stream()  # eager DP step: critical path on its own HW queue
         self._graph: Optional[StepGraph] = None
         self._metrics_cache = None
         self.cur_lr = float("nan")

@@ -10,6 +10,6 @@ for v in "$@"; do
   line=$(env $v timeout -k 10 120 python bench.py --steps ${SWEEP_STEPS:-40} --warmup 5 ${SWEEP_ARGS:-} 2>>"$OUT.err")
   rc=$?
   if [ $rc -ne 0 ]; then echo "variant [$v] failed rc=$rc" | tee -a "$OUT"; exit $rc; fi
-  ms=$(echo "$line" | python -c 'import json,sys; print(json.loads(sys.stdin.read())["ms_per_step"])')
+  ms=$(echo "$line" | python -c 'import json,sys; print(json.loads([l for l in sys.stdin.read().splitlines() if l.startswith("{")][-1])["ms_per_step"])')
   echo "$ms ms  [$v]" | tee -a "$OUT"
 done
