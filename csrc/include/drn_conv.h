@@ -11,6 +11,13 @@ struct DrnFastDiv {
   uint32_t d, m, s, pad_;
 };
 
+#if defined(__HIPCC__)
+// n / f.d for n < 2^31 in 3 VALU ops (a runtime-divisor integer division is ~40)
+__device__ __forceinline__ uint32_t drn_fdiv(uint32_t n, const DrnFastDiv& f) {
+  return (__umulhi(n, f.m) + n) >> f.s;
+}
+#endif
+
 // y[N][P][Q][K] = conv(x[N][H][W][C], w[K][R][S][C])  (NHWC / KRSC, bf16, fp32 accumulate)
 //
 // The same kernel runs the data-gradient of a convolution as a forward convolution of dY with
@@ -72,6 +79,8 @@ struct DrnConvFwdArgs {
   float* fin_dgamma;
   float* fin_dbeta;
   float* fin_coef;
+  // pixel-index decode m -> (n, p, q): divisors P*Q and Q (filled by the host)
+  DrnFastDiv fd_pq, fd_q;
 };
 
 // dW[K][R][S][C] (+)= sum_{n,p,q} dy[n,p,q,k] * x[n, p*st-pad+r, q*st-pad+s, c]

@@ -60,9 +60,9 @@ __device__ __forceinline__ void epi_prefetch(const DrnConvFwdArgs& a, int m0, in
     int off = -1;
     if (m < M && c < a.K) {
       if (mapped) {
-        const int n = m / pq;
+        const int n = (int)drn_fdiv((uint32_t)m, a.fd_pq);
         const int rem = m - n * pq;
-        const int i = rem / a.Q;
+        const int i = (int)drn_fdiv((uint32_t)rem, a.fd_q);
         const int j = rem - i * a.Q;
         off = ((n * a.out_H + i * a.out_stride + a.out_oh) * a.out_W + j * a.out_stride + a.out_ow) * a.K + c;
       } else {
@@ -218,9 +218,9 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
           // zeros at this pixel's sibling phase positions (single-phase strided output)
           const int m = m0 + row;
           const int pq = a.P * a.Q;
-          const int n = m / pq;
+          const int n = (int)drn_fdiv((uint32_t)m, a.fd_pq);
           const int rem = m - n * pq;
-          const int i = rem / a.Q;
+          const int i = (int)drn_fdiv((uint32_t)rem, a.fd_q);
           const int j = rem - i * a.Q;
           for (int ph = 0; ph < a.out_stride; ++ph)
             for (int pw = 0; pw < a.out_stride; ++pw) {
@@ -301,9 +301,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(DrnConvFwdArgs a) {
     const int m = m0 + row;
     if (m < M) {
       const int pq = a.P * a.Q;
-      const int n = m / pq;
+      const int n = (int)drn_fdiv((uint32_t)m, a.fd_pq);
       const int rem = m - n * pq;
-      const int p = rem / a.Q;
+      const int p = (int)drn_fdiv((uint32_t)rem, a.fd_q);
       const int q = rem - p * a.Q;
       b_base[i] = n * a.H * a.W * a.C;
       b_h[i] = p * a.stride - a.pad_h;
@@ -576,9 +576,9 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
     const int m = m0 + row;
     if (m < M) {
       const int pq = a.P * a.Q;
-      const int n = m / pq;
+      const int n = (int)drn_fdiv((uint32_t)m, a.fd_pq);
       const int rem = m - n * pq;
-      const int p = rem / a.Q;
+      const int p = (int)drn_fdiv((uint32_t)rem, a.fd_q);
       const int q = rem - p * a.Q;
       bh[i] = p * a.stride - a.pad_h;
       bw[i] = q * a.stride - a.pad_w;

@@ -29,9 +29,7 @@
 
 namespace drn {
 
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const DrnFastDiv& f) {
-  return (__umulhi(n, f.m) + n) >> f.s;
-}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const DrnFastDiv& f) { return drn_fdiv(n, f); }
 
 // 32-byte-slot swizzle for rows of W bytes (W = 128 or 256)
 template <int W>

@@ -51,6 +51,7 @@ class DrnConvFwdArgs(ctypes.Structure):
         ("fin_gamma", c_p), ("fin_beta", c_p), ("fin_run_mean", c_p), ("fin_run_var", c_p),
         ("fin_scale", c_p), ("fin_shift", c_p), ("fin_mean", c_p), ("fin_invstd", c_p),
         ("fin_dgamma", c_p), ("fin_dbeta", c_p), ("fin_coef", c_p),
+        ("fd_pq", DrnFastDiv), ("fd_q", DrnFastDiv),
     ]
 
 

@@ -191,6 +191,8 @@ class HipBackend(_Common):
         a.stats = _ptr(stats)
         a.N, a.H, a.W, a.C, a.K, a.R, a.S, a.P, a.Q = N, H, W, C, K, R, S, P, Q
         a.stride, a.pad_h, a.pad_w, a.dil = g.stride, g.pad_h, g.pad_w, g.dil
+        a.fd_pq = _lib.DrnFastDiv.make(P * Q)
+        a.fd_q = _lib.DrnFastDiv.make(Q)
         a.relu_in = 1 if relu_in else 0
         if out_map is not None:
             a.out_H, a.out_W, a.out_stride, a.out_oh, a.out_ow = oH, oW, out_map.stride, out_map.oh, out_map.ow
