@@ -43,15 +43,20 @@ __global__ __launch_bounds__(256) void bnrelu_pool_kernel(const bf16_t* __restri
 // C[M][N] = alpha * op(A) op(B) + beta * C (+ bias[N]); row-major; op = transpose if flag.
 // Exact-fp32 MFMA (v_mfma_f32_16x16x4_f32, the f32-input matrix path: 16x the VALU-FMA work
 // per instruction, bitwise a k-ordered fmaf chain). 64x64 block tile, 4 waves each 32x32
-// (2x2 MFMA tiles), K staged 32 at a time through LDS ([k][m] and [k][n], +1 padding).
+// (2x2 MFMA tiles), K staged 32 at a time through double-buffered LDS ([k][m] and [k][n], +1
+// padding): the next slab's global loads are issued into registers before the current slab's
+// MFMAs and stored to the other buffer after them (one barrier per slab), so their latency
+// hides behind the MFMA chain -- the unpipelined load/barrier/MFMA loop, one workgroup per CU,
+// was latency-bound (60 us for the 0.5 GFLOP ResNet-50 logits GEMM).
 // Used for the dense layer of the head (logits, dW, dpool: <1 GFLOP each).
 __global__ __launch_bounds__(256) void sgemm_kernel(int ta, int tb, int M, int N, int K, float alpha,
                                                     const float* __restrict__ A, int lda,
                                                     const float* __restrict__ B, int ldb, float beta,
                                                     float* __restrict__ Cm, int ldc, const float* __restrict__ bias) {
   constexpr int BM = 64, BN = 64, BK = 32;
-  __shared__ float As[BK][BM + 1];
-  __shared__ float Bs[BK][BN + 1];
+  constexpr int LA = BK * BM / 256, LB = BK * BN / 256;  // slab elements per thread
+  __shared__ float As[2][BK][BM + 1];
+  __shared__ float Bs[2][BK][BN + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int wm = (wave & 1) * 32, wn = (wave >> 1) * 32;
@@ -70,35 +75,60 @@ __global__ __launch_bounds__(256) void sgemm_kernel(int ta, int tb, int M, int N
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  for (int k0 = kb; k0 < ke; k0 += BK) {
-    for (int t = tid; t < BK * BM; t += 256) {
-      int kk, mm;
-      if (ta) { mm = t % BM; kk = t / BM; } else { kk = t % BK; mm = t / BK; }
+  // element t of a slab: A at [k][m] = (t / BM, t % BM) when transposed (m contiguous in
+  // memory), else (t % BK, t / BK) (k contiguous); likewise B with n
+  float ra[LA], rb[LB];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int t = tid + 256 * i;
+      const int kk = ta ? t / BM : t % BK, mm = ta ? t % BM : t / BK;
       const int gm = m0 + mm, gk = k0 + kk;
-      float v = 0.f;
-      if (gm < M && gk < ke) v = ta ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk];
-      As[kk][mm] = v;
+      ra[i] = (gm < M && gk < ke) ? (ta ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk]) : 0.f;
     }
-    for (int t = tid; t < BK * BN; t += 256) {
-      int kk, nn;
-      if (tb) { kk = t % BK; nn = t / BK; } else { nn = t % BN; kk = t / BN; }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int t = tid + 256 * i;
+      const int kk = tb ? t % BK : t / BN, nn = tb ? t / BK : t % BN;
       const int gn = n0 + nn, gk = k0 + kk;
-      float v = 0.f;
-      if (gn < N && gk < ke) v = tb ? B[(size_t)gn * ldb + gk] : B[(size_t)gk * ldb + gn];
-      Bs[kk][nn] = v;
+      rb[i] = (gn < N && gk < ke) ? (tb ? B[(size_t)gn * ldb + gk] : B[(size_t)gk * ldb + gn]) : 0.f;
     }
-    __syncthreads();
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < LA; ++i) {
+      const int t = tid + 256 * i;
+      As[buf][ta ? t / BM : t % BK][ta ? t % BM : t / BK] = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int t = tid + 256 * i;
+      Bs[buf][tb ? t % BK : t / BN][tb ? t / BK : t % BN] = rb[i];
+    }
+  };
+  if (kb < ke) {
+    load(kb);
+    store(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int k0 = kb; k0 < ke; k0 += BK) {
+    const bool more = k0 + BK < ke;
+    if (more) load(k0 + BK);  // in flight during this slab's MFMAs
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
       const int kr = kk + (lane >> 4);
-      float a0 = As[kr][wm + (lane & 15)], a1 = As[kr][wm + 16 + (lane & 15)];
-      float b0 = Bs[kr][wn + (lane & 15)], b1 = Bs[kr][wn + 16 + (lane & 15)];
+      float a0 = As[buf][kr][wm + (lane & 15)], a1 = As[buf][kr][wm + 16 + (lane & 15)];
+      float b0 = Bs[buf][kr][wn + (lane & 15)], b1 = Bs[buf][kr][wn + 16 + (lane & 15)];
       acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
       acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
       acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
       acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
     }
+    // the other buffer was last read before the previous barrier: safe to overwrite
+    if (more) store(buf ^ 1);
     __syncthreads();
+    buf ^= 1;
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i)

@@ -470,10 +470,11 @@ class HipBackend(_Common):
                                           1 if relu else 0, self.stream()), "drn_bnrelu_pool")
 
     _sgemm_ws = None
+    SGEMM_TARGET_WG = int(os.environ.get("DRN_SGEMM_TARGET_WG", "256"))
 
     def sgemm(self, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias=None):
         tiles = ((M + 63) // 64) * ((N + 63) // 64)
-        splits = max(1, min(K // 128, 256 // max(tiles, 1)))  # fill >= ~256 CUs on long-K GEMMs
+        splits = max(1, min(K // 128, self.SGEMM_TARGET_WG // max(tiles, 1)))  # fill the CUs on long-K GEMMs
         ws = None
         if splits > 1:
             need = splits * M * ldc
@@ -497,11 +498,13 @@ class HipBackend(_Common):
                                      self.stream()), "drn_colsum")
 
     # -- pooling --------------------------------------------------------------------------------
-    def maxpool_fwd(self, x, y, arg, k, stride, pad_h, pad_w):
+    def maxpool_fwd(self, x, y, arg, k, stride, pad_h, pad_w, stats=None):
+        """stats (optional [R][2][C] fp32): += per-channel (sum, sumsq) of y, fused in the kernel."""
         N, H, W, C = x.shape
         _, P, Q, _ = y.shape
+        rep = stats.numel() // (2 * C) if stats is not None else 0
         _lib.check(self.L.drn_maxpool_fwd(x.data_ptr(), y.data_ptr(), arg.data_ptr(), N, H, W, C, P, Q, k, stride,
-                                          pad_h, pad_w, self.stream()), "drn_maxpool_fwd")
+                                          pad_h, pad_w, _ptr(stats), rep, self.stream()), "drn_maxpool_fwd")
 
     def maxpool_bwd(self, dy, arg, dx, k, stride, pad_h, pad_w):
         N, H, W, C = dx.shape
@@ -762,7 +765,12 @@ class RefBackend(_Common):
         else:
             out.copy_(s)
 
-    def maxpool_fwd(self, x, y, arg, k, stride, pad_h, pad_w):
+    def maxpool_fwd(self, x, y, arg, k, stride, pad_h, pad_w, stats=None):
+        self._maxpool_fwd(x, y, arg, k, stride, pad_h, pad_w)
+        if stats is not None:
+            self.bn_stats(y, stats)
+
+    def _maxpool_fwd(self, x, y, arg, k, stride, pad_h, pad_w):
         N, H, W, C = x.shape
         _, P, Q, _ = y.shape
         xc = x.to(_DT[0]).permute(0, 3, 1, 2)

@@ -466,8 +466,12 @@ class Executor:
         if sp.maxpool:
             ph = sp.pool_hw
             pad = max((ph - 1) * 2 + 3 - sp.stem_hw, 0) // 2
-            be.maxpool_fwd(self.stem_out, self.pool_out, self.pool_arg, 3, 2, pad, pad)
-            if train:
+            # the first block's BN statistics come out of the pooling kernel itself (the
+            # deterministic mode keeps the separate one-replica-per-block statistics pass)
+            fused = train and not self.deterministic
+            be.maxpool_fwd(self.stem_out, self.pool_out, self.pool_arg, 3, 2, pad, pad,
+                           stats=self.pool_stats if fused else None)
+            if train and not fused:
                 be.bn_stats(self.pool_out, self.pool_stats)
         for bp in self.blocks:
             self._block_fwd(bp, train)

@@ -426,12 +426,14 @@ def test_maxpool(hip, ref, H, pad):
         xx = x.cuda() if dev == "cuda" else x.float()
         y = torch.zeros(N, P, P, C, dtype=xx.dtype, device=dev)
         arg = torch.zeros(N, P, P, C, dtype=torch.uint8, device=dev)
-        be.maxpool_fwd(xx, y, arg, 3, 2, pad, pad)
+        st = torch.zeros(3, 2, C, device=dev)  # fused output statistics, 3 atomic replicas
+        be.maxpool_fwd(xx, y, arg, 3, 2, pad, pad, stats=st)
         dx = torch.full_like(xx, 3.0)
         be.maxpool_bwd(dy.to(dev) if dev == "cuda" else dy.float(), arg, dx, 3, 2, pad, pad)
-        out[be.name] = [y.float().cpu(), arg.cpu(), dx.float().cpu()]
+        out[be.name] = [y.float().cpu(), arg.cpu(), dx.float().cpu(), st.sum(0).cpu()]
     assert rel(out["hip"][0], out["ref"][0]) < 1e-3
     assert rel(out["hip"][2], out["ref"][2]) < 1e-2
+    assert rel(out["hip"][3], out["ref"][3]) < 1e-3
 
 
 def test_sgd_and_tflip(hip, ref):
