@@ -469,7 +469,7 @@ class HipBackend(_Common):
         _lib.check(self.L.drn_bnrelu_pool(x.data_ptr(), _ptr(scale), _ptr(shift), pooled.data_ptr(), N, H * W, C,
                                           1 if relu else 0, self.stream()), "drn_bnrelu_pool")
 
-    _sgemm_ws = None
+    _sgemm_ws: dict = {}
     SGEMM_TARGET_WG = int(os.environ.get("DRN_SGEMM_TARGET_WG", "256"))
 
     def sgemm(self, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias=None):
@@ -477,11 +477,14 @@ class HipBackend(_Common):
         splits = max(1, min(K // 128, self.SGEMM_TARGET_WG // max(tiles, 1)))  # fill the CUs on long-K GEMMs
         ws = None
         if splits > 1:
+            # split-K partials: one workspace per stream (GEMMs on the weight-gradient side
+            # stream run concurrently with the main stream's)
             need = splits * M * ldc
-            if HipBackend._sgemm_ws is None or HipBackend._sgemm_ws.numel() < need \
-                    or HipBackend._sgemm_ws.device != C.device:
-                HipBackend._sgemm_ws = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=C.device)
-            ws = HipBackend._sgemm_ws
+            key = (C.device, self.stream())
+            ws = HipBackend._sgemm_ws.get(key)
+            if ws is None or ws.numel() < need:
+                ws = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=C.device)
+                HipBackend._sgemm_ws[key] = ws
         _lib.check(self.L.drn_sgemm(int(ta), int(tb), M, N, K, float(alpha), A.data_ptr(), lda, B.data_ptr(), ldb,
                                     float(beta), C.data_ptr(), ldc, _ptr(bias), splits, _ptr(ws), self.stream()),
                    "drn_sgemm")

@@ -550,9 +550,16 @@ class Executor:
     def backward(self):
         be, sp = self.be, self.spec
         N, C, ncls = self.N, sp.final_c, sp.num_classes
-        # dense layer
-        be.sgemm(1, 0, ncls, C, N, 1.0, self.dlogits, ncls, self.pooled, C, 0.0, self.dense_dw, C)
-        be.colsum(self.dlogits, self.dense_db)
+        # dense layer: its weight / bias gradients only feed the optimizer, so with the side
+        # stream they run there, off the data-gradient chain
+        if self.side is not None:
+            self.side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.side):
+                be.sgemm(1, 0, ncls, C, N, 1.0, self.dlogits, ncls, self.pooled, C, 0.0, self.dense_dw, C)
+                be.colsum(self.dlogits, self.dense_db)
+        else:
+            be.sgemm(1, 0, ncls, C, N, 1.0, self.dlogits, ncls, self.pooled, C, 0.0, self.dense_dw, C)
+            be.colsum(self.dlogits, self.dense_db)
         be.sgemm(0, 0, N, C, ncls, 1.0, self.dlogits, ncls, self.dense_w, C, 0.0, self.dpool, C)
         fb = self.final_bn
         hw = self.last_out.shape[1] * self.last_out.shape[2]
