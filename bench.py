@@ -68,7 +68,7 @@ def main():
     if force_dp and world == 1 and "MASTER_ADDR" not in os.environ:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("DRN_BENCH_PORT", "29533"),
                           RANK="0", WORLD_SIZE="1")
-    if (world > 1 or force_dp) and args.graph != 1:
+    if (world > 1 or force_dp or args.graph == 0) and args.graph != 1:
         # eager data-parallel step: its main (critical-path) stream at HIGH priority -- see
         # parallel.engine.use_priority_main_stream
         from distributed_resnet_tensorflow_amd.parallel.engine import use_priority_main_stream
@@ -126,6 +126,22 @@ def main():
     elif use_graph:
         sg = StepGraph(step, warmup=2)
         run = sg.replay
+        if args.graph == -1:
+            # auto: keep whichever of graph replay and eager launches is faster for this step
+            # (untimed, before the warm-up). Short steps (CIFAR, 2.8 ms) are host-launch-bound
+            # eager (5.3 ms); the ResNet-50 ImageNet step measured faster eager (10.55 vs 10.85
+            # ms): the host stays ahead and the replay adds gaps around the side-stream branches
+            def _time(fn, n=5):
+                fn()
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                for _ in range(n):
+                    fn()
+                torch.cuda.synchronize()
+                return time.perf_counter() - t
+
+            if _time(step) < _time(sg.replay):
+                run, use_graph = step, 0
     for _ in range(args.warmup):
         run()
     torch.cuda.synchronize()

@@ -263,6 +263,12 @@ struct DySrc {
       unpack8(*reinterpret_cast<const uint4*>(dy + m * C + c), f);
     }
   }
+  // the same for flat 16-byte vector index i = m * (C/8) + c/8 with C/8 = 1 << cv_shift (the
+  // streaming kernels' grid-stride index): no 64-bit division in the loop
+  __device__ __forceinline__ void load_vec(int64_t i, int cv_shift, int C, int c, float* f) const {
+    if (pool_hw > 0) load(i >> cv_shift, C, c, f);
+    else unpack8(reinterpret_cast<const uint4*>(dy)[i], f);
+  }
 };
 
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(DySrc src, const bf16_t* __restrict__ x,
@@ -350,6 +356,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(DySrc src, const bf16
   const int CV = C / 8;
   const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int c = (int)(i0 & (CV - 1)) * 8;
+  const int cv_shift = __ffs(CV) - 1;
   float sc[8], sh[8], A[8], B[8], D[8];
   {
     float mu[8], is[8], k1[8], k2[8], k3[8];
@@ -368,10 +375,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(DySrc src, const bf16
     }
   }
   for (int64_t i = i0; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t m = i / CV;
     float fx[8], fd[8], fa[8];
     unpack8(reinterpret_cast<const uint4*>(x)[i], fx);
-    src.load(m, C, c, fd);
+    src.load_vec(i, cv_shift, C, c, fd);
     if (add) unpack8(reinterpret_cast<const uint4*>(add)[i], fa);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -394,6 +400,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_stats_kernel(
   const int CV = C / 8;
   const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int c = (int)(i0 & (CV - 1)) * 8;  // CV is a power of two
+  const int cv_shift = __ffs(CV) - 1;
   float sg[8], sgx[8], ga[8], k1[8], k2[8], k3[8], sc[8], sh[8], mu[8], is[8];
   load8f(acc + c, sg);
   load8f(acc + C + c, sgx);
@@ -413,10 +420,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_stats_kernel(
     store8f(dgamma + c, sgx);
   }
   for (int64_t i = i0; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t m = i / CV;
     float fx[8], fd[8], fa[8];
     unpack8(reinterpret_cast<const uint4*>(x)[i], fx);
-    src.load(m, C, c, fd);
+    src.load_vec(i, cv_shift, C, c, fd);
     if (add) unpack8(reinterpret_cast<const uint4*>(add)[i], fa);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
