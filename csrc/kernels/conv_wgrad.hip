@@ -581,32 +581,37 @@ static int dispatch_wgrad_glds(DrnConvWgradArgs* a, const void* zero, int ns, hi
   }
 }
 
-// out[i] (+)= scale * sum_k ws[k][i]: block = 64 float4 columns x 4 split-groups; every
-// thread keeps 4 independent loads in flight (the split loop is the latency chain for small
-// tensors with many splits), then the 4 groups are summed through LDS in a fixed order
-// (deterministic).
+// out[i] (+)= scale * sum_k ws[k][i]: block = COLS float4 columns x (256/COLS) split-groups;
+// every thread keeps 4 independent loads in flight (the split loop is the latency chain for
+// small tensors with many splits), then the groups are combined by a fixed-order LDS tree
+// (deterministic). Small outputs with many splits (early-stage layers: 1-9K float4 x 100-500
+// splits) take COLS = 4/16 so the grid still spreads over the CUs instead of a few blocks
+// walking hundreds of splits each.
+__device__ __forceinline__ void f4_add(float4& s, const float4 a) {
+  s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+}
+
+template <int COLS>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ out,
                                                             int n4, int splits, size_t stride4, float scale,
                                                             int accumulate) {
-  __shared__ float4 red[4][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int i = blockIdx.x * 64 + tx;
+  constexpr int G = 256 / COLS;
+  __shared__ float4 red[G][COLS];
+  const int tx = threadIdx.x % COLS, ty = threadIdx.x / COLS;
+  const int i = blockIdx.x * COLS + tx;
   float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0, s2 = s0, s3 = s0;
   if (i < n4) {
     const float4* p = reinterpret_cast<const float4*>(ws) + i;
     int k = ty;
-    for (; k + 12 < splits; k += 16) {
-      const float4 a = p[(size_t)k * stride4], b = p[(size_t)(k + 4) * stride4];
-      const float4 c = p[(size_t)(k + 8) * stride4], d = p[(size_t)(k + 12) * stride4];
-      s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
-      s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
-      s2.x += c.x; s2.y += c.y; s2.z += c.z; s2.w += c.w;
-      s3.x += d.x; s3.y += d.y; s3.z += d.z; s3.w += d.w;
+    for (; k + 3 * G < splits; k += 4 * G) {
+      const float4 a = p[(size_t)k * stride4], b = p[(size_t)(k + G) * stride4];
+      const float4 c = p[(size_t)(k + 2 * G) * stride4], d = p[(size_t)(k + 3 * G) * stride4];
+      f4_add(s0, a);
+      f4_add(s1, b);
+      f4_add(s2, c);
+      f4_add(s3, d);
     }
-    for (; k < splits; k += 4) {
-      const float4 a = p[(size_t)k * stride4];
-      s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
-    }
+    for (; k < splits; k += G) f4_add(s0, p[(size_t)k * stride4]);
   }
   float4 t;
   t.x = (s0.x + s1.x) + (s2.x + s3.x);
@@ -615,12 +620,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   t.w = (s0.w + s1.w) + (s2.w + s3.w);
   red[ty][tx] = t;
   __syncthreads();
+#pragma unroll
+  for (int w = G / 2; w >= 1; w >>= 1) {
+    if (ty < w) {
+      float4 u = red[ty][tx];
+      f4_add(u, red[ty + w][tx]);
+      red[ty][tx] = u;
+    }
+    __syncthreads();
+  }
   if (ty == 0 && i < n4) {
     float4 r = red[0][tx];
-#pragma unroll
-    for (int g = 1; g < 4; ++g) {
-      r.x += red[g][tx].x; r.y += red[g][tx].y; r.z += red[g][tx].z; r.w += red[g][tx].w;
-    }
     r.x *= scale; r.y *= scale; r.z *= scale; r.w *= scale;
     if (accumulate) {
       const float4 o = reinterpret_cast<float4*>(out)[i];
@@ -658,8 +668,18 @@ DRN_API int drn_splitk_reduce(const float* ws, float* out, int64_t n, int splits
                               hipStream_t s) {
   if (n % 4) return (int)hipErrorInvalidValue;
   const int n4 = (int)(n / 4);
-  const int blocks = (n4 + 63) / 64;
-  hipLaunchKernelGGL(drn::splitk_reduce_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, s, ws, out, n4, splits,
-                     (size_t)n4, scale, accumulate);
+  // widest column tile that still gives >= 512 blocks (2 per CU), or whose split-groups
+  // would otherwise idle (splits <= groups)
+  const int cols = (n4 >= 512 * 64 || splits <= 8) ? 64 : (n4 >= 512 * 16 || splits <= 32) ? 16 : 4;
+  const int blocks = n4 > 0 ? (n4 + cols - 1) / cols : 1;
+  if (cols == 64)
+    hipLaunchKernelGGL(drn::splitk_reduce_kernel<64>, dim3(blocks), dim3(256), 0, s, ws, out, n4, splits, (size_t)n4,
+                       scale, accumulate);
+  else if (cols == 16)
+    hipLaunchKernelGGL(drn::splitk_reduce_kernel<16>, dim3(blocks), dim3(256), 0, s, ws, out, n4, splits, (size_t)n4,
+                       scale, accumulate);
+  else
+    hipLaunchKernelGGL(drn::splitk_reduce_kernel<4>, dim3(blocks), dim3(256), 0, s, ws, out, n4, splits, (size_t)n4,
+                       scale, accumulate);
   return (int)hipGetLastError();
 }

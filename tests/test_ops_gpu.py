@@ -295,6 +295,27 @@ def test_conv_wgrad_large_splitk(hip, ref):
     assert rel(dw, dw_ref) < 1e-2
 
 
+@pytest.mark.parametrize("n,splits", [(4096, 483), (36864, 103), (25088, 128), (147456, 36), (1048576, 4),
+                                      (1024, 7), (64, 1), (8, 300)])
+@pytest.mark.parametrize("accumulate", [0, 1])
+def test_splitk_reduce(hip, n, splits, accumulate):
+    """Deterministic split-K reduction (all three column-tile widths) vs an fp64 sum."""
+    torch.manual_seed(11)
+    ws = torch.randn(splits, n, device="cuda")
+    out0 = torch.randn(n, device="cuda")
+    out = out0.clone()
+    from distributed_resnet_tensorflow_amd.ops import _lib
+    _lib.check(hip.L.drn_splitk_reduce(ws.data_ptr(), out.data_ptr(), n, splits, 0.5, accumulate, hip.stream()),
+               "drn_splitk_reduce")
+    again = out0.clone()
+    _lib.check(hip.L.drn_splitk_reduce(ws.data_ptr(), again.data_ptr(), n, splits, 0.5, accumulate, hip.stream()),
+               "drn_splitk_reduce")
+    torch.cuda.synchronize()
+    want = 0.5 * ws.double().sum(0) + (out0.double() if accumulate else 0)
+    assert (out.double() - want).abs().max().item() < 1e-4 * max(1.0, splits ** 0.5)
+    assert torch.equal(out, again)  # bitwise reproducible
+
+
 @pytest.mark.parametrize("C", [16, 64, 256, 2048])
 def test_bn_forward_and_backward(hip, ref, C):
     torch.manual_seed(4)
