@@ -24,8 +24,29 @@ def _flags(**defaults):
     return fv
 
 
+# per-entry-point flag defaults (the reference scripts' own DEFINE_* defaults)
+ENTRY_DEFAULTS = {
+    "cifar_main": dict(dataset="cifar10", batch_size=32, train_steps=2000, log_every_n_steps=20),
+    "cifar_horovod_main": dict(dataset="cifar10", batch_size=32, train_steps=2000, log_every_n_steps=20,
+                               use_horovod=True),
+    "imagenet_main": dict(dataset="imagenet", batch_size=128, train_steps=200, log_every_n_steps=40,
+                          image_size=224, num_epochs=90),
+    "cifar_eval_main": dict(dataset="cifar10", mode="eval"),
+    "imagenet_eval_main": dict(dataset="imagenet", mode="eval", batch_size=128, num_epochs=3000, image_size=224),
+    "single_main": dict(dataset="cifar10", batch_size=128, train_steps=2000, log_every_n_steps=100,
+                        resnet_size=20),
+}
+
+
+def entry_flags(entry: str, argv=None):
+    """Parsed flags of an entry point (`argv` without the program name)."""
+    FLAGS = _flags(**ENTRY_DEFAULTS[entry])
+    FLAGS([entry] + list(sys.argv[1:] if argv is None else argv))
+    return FLAGS
+
+
 def cifar_main(argv=None):
-    FLAGS = _flags(dataset="cifar10", batch_size=32, train_steps=2000, log_every_n_steps=20)
+    FLAGS = _flags(**ENTRY_DEFAULTS["cifar_main"])
     FLAGS(list(sys.argv if argv is None else argv))
     from .train.trainer import train
     if FLAGS.mode != "train":
@@ -34,7 +55,7 @@ def cifar_main(argv=None):
 
 
 def cifar_horovod_main(argv=None):
-    FLAGS = _flags(dataset="cifar10", batch_size=32, train_steps=2000, log_every_n_steps=20, use_horovod=True)
+    FLAGS = _flags(**ENTRY_DEFAULTS["cifar_horovod_main"])
     FLAGS(list(sys.argv if argv is None else argv))
     FLAGS.use_horovod = True
     from .train.trainer import train
@@ -42,15 +63,14 @@ def cifar_horovod_main(argv=None):
 
 
 def imagenet_main(argv=None):
-    FLAGS = _flags(dataset="imagenet", batch_size=128, train_steps=200, log_every_n_steps=40, image_size=224,
-                   num_epochs=90)
+    FLAGS = _flags(**ENTRY_DEFAULTS["imagenet_main"])
     FLAGS(list(sys.argv if argv is None else argv))
     from .train.trainer import train
     return train(FLAGS)
 
 
 def cifar_eval_main(argv=None):
-    FLAGS = _flags(dataset="cifar10", mode="eval")
+    FLAGS = _flags(**ENTRY_DEFAULTS["cifar_eval_main"])
     FLAGS(list(sys.argv if argv is None else argv))
     from .train.evaluator import evaluate
     evaluate(FLAGS, eval_batch_size=100)
@@ -58,7 +78,7 @@ def cifar_eval_main(argv=None):
 
 
 def imagenet_eval_main(argv=None):
-    FLAGS = _flags(dataset="imagenet", mode="eval", batch_size=128, num_epochs=3000, image_size=224)
+    FLAGS = _flags(**ENTRY_DEFAULTS["imagenet_eval_main"])
     FLAGS(list(sys.argv if argv is None else argv))
     from .train.evaluator import evaluate
     evaluate(FLAGS, eval_batch_size=FLAGS.batch_size)
@@ -66,7 +86,7 @@ def imagenet_eval_main(argv=None):
 
 
 def single_main(argv=None):
-    FLAGS = _flags(dataset="cifar10", batch_size=128, train_steps=2000, log_every_n_steps=100, resnet_size=20)
+    FLAGS = _flags(**ENTRY_DEFAULTS["single_main"])
     FLAGS(list(sys.argv if argv is None else argv))
     if FLAGS.mode == "eval":
         from .train.evaluator import evaluate

@@ -88,17 +88,35 @@ class CifarRecords:
         images[:] = recs[:, self.label_bytes:].reshape(-1, DEPTH, HEIGHT, WIDTH).transpose(0, 2, 3, 1)
 
 
+def _host_array(shape, dtype, pin: bool):
+    """(tensor-or-array, numpy view) of a fresh host buffer; page-locked when `pin`."""
+    if not pin:
+        a = np.empty(shape, dtype=dtype)
+        return a, a
+    import torch
+    t = torch.empty(shape, dtype={np.uint8: torch.uint8, np.int32: torch.int32}[dtype], pin_memory=True)
+    return t, t.numpy()
+
+
 class CifarLoader:
     """Iterator of (uint8 HWC images, int32 labels, int32 aug params [n,3]) host batches.
 
     Train: epoch-wise shuffled, rank-sharded, drop-remainder; random crop offsets in [0, 2*PAD]
     and flip bits drawn from the seeded host RNG. Eval: sequential, no augmentation.
-    A background thread keeps `prefetch` batches ready.
+    A background thread keeps `prefetch` batches ready. With `pin=True` every batch is gathered
+    straight into its own page-locked tensors (PyTorch's caching host allocator does not hand a
+    block out again until the async copies recorded on it have completed, so a batch can never
+    be overwritten while its DMA is in flight). Each batch carries the loader position *after*
+    it (`state()` reports the position after the last batch handed out) and its number of
+    valid (non-wrapped) images (`valid`: only the final partial eval batch has fewer).
     """
 
     def __init__(self, records: CifarRecords, batch_size: int, is_training: bool, seed: int = 0, rank: int = 0,
-                 world: int = 1, prefetch: int = 4, epoch: int = 0, cursor: int = 0):
+                 world: int = 1, prefetch: int = 4, epoch: int = 0, cursor: int = 0, pin: bool = False,
+                 pin_device=None):
         self.rec = records
+        self.pin, self.pin_device = pin, pin_device
+        self.valid = batch_size
         self.bs = batch_size
         self.train = is_training
         self.seed, self.rank, self.world = seed, rank, world
@@ -117,32 +135,39 @@ class CifarLoader:
         return p[self.rank * per:(self.rank + 1) * per]
 
     def _run(self):
+        if self.pin and self.pin_device is not None:
+            import torch
+            torch.cuda.set_device(self.pin_device)  # page-locked allocations in this rank's context
         epoch, cursor = self.epoch, self.cursor
         perm = self._perm(epoch)
-        rng = np.random.default_rng([self.seed, 7919, self.rank, epoch, cursor])
         while not self._stop.is_set():
+            valid = self.bs
             if cursor + self.bs > len(perm):
                 if not self.train and cursor < len(perm):
-                    idx = perm[cursor:]  # final partial eval batch
+                    idx = perm[cursor:]  # final partial eval batch, padded by wrapping around
+                    valid = len(idx)
                     idx = np.concatenate([idx, perm[:self.bs - len(idx)]])
                 else:
                     epoch += 1
                     cursor = 0
                     perm = self._perm(epoch)
-                    rng = np.random.default_rng([self.seed, 7919, self.rank, epoch, 0])
                     continue
             else:
                 idx = perm[cursor:cursor + self.bs]
+            # crop/flip draws are a function of the batch position: a resumed loader is exact
+            rng = np.random.default_rng([self.seed, 7919, self.rank, epoch, cursor])
             cursor += self.bs
-            imgs = np.empty((self.bs, HEIGHT, WIDTH, DEPTH), dtype=np.uint8)
-            labels = np.empty((self.bs,), dtype=np.int32)
-            self.rec.gather(idx, imgs, labels)
+            imgs, imgs_np = _host_array((self.bs, HEIGHT, WIDTH, DEPTH), np.uint8, self.pin)
+            labels, labels_np = _host_array((self.bs,), np.int32, self.pin)
+            self.rec.gather(idx, imgs_np, labels_np)
             if self.train:
-                params = np.stack([rng.integers(0, 2 * PAD + 1, self.bs), rng.integers(0, 2 * PAD + 1, self.bs),
-                                   rng.integers(0, 2, self.bs)], axis=1).astype(np.int32)
+                p = np.stack([rng.integers(0, 2 * PAD + 1, self.bs), rng.integers(0, 2 * PAD + 1, self.bs),
+                              rng.integers(0, 2, self.bs)], axis=1).astype(np.int32)
             else:
-                params = np.tile(np.array([[PAD, PAD, 0]], dtype=np.int32), (self.bs, 1))
-            item = (imgs, labels, params, epoch, cursor)
+                p = np.tile(np.array([[PAD, PAD, 0]], dtype=np.int32), (self.bs, 1))
+            params, params_np = _host_array((self.bs, 3), np.int32, self.pin)
+            params_np[...] = p
+            item = (imgs, labels, params, epoch, cursor, valid)
             while not self._stop.is_set():
                 try:
                     self.q.put(item, timeout=0.1)
@@ -154,8 +179,8 @@ class CifarLoader:
         return self
 
     def __next__(self):
-        imgs, labels, params, epoch, cursor = self.q.get()
-        self.epoch, self.cursor = epoch, cursor
+        imgs, labels, params, epoch, cursor, valid = self.q.get()
+        self.epoch, self.cursor, self.valid = epoch, cursor, valid
         return imgs, labels, params
 
     def state(self):
@@ -166,8 +191,12 @@ class CifarLoader:
         self._t.join(timeout=2)
 
 
-def write_fake_cifar(dirpath: str, n_per_file: int = 100, dataset: str = "cifar10", seed: int = 0) -> str:
-    """Writes small CIFAR-format binary files (tests / smoke runs without the real dataset)."""
+def write_fake_cifar(dirpath: str, n_per_file: int = 100, dataset: str = "cifar10", seed: int = 0,
+                     learnable: bool = False) -> str:
+    """Writes small CIFAR-format binary files (tests / smoke runs without the real dataset).
+    `learnable`: every class has its own colour (per-channel offsets that survive the per-image
+    standardisation, crops and flips) plus noise, so a trained model can reach high precision
+    on the test file — a convergence check with no dataset available."""
     rng = np.random.default_rng(seed)
     lb, lo = record_layout(dataset)
     ncls = 100 if dataset == "cifar100" else 10
@@ -184,8 +213,15 @@ def write_fake_cifar(dirpath: str, n_per_file: int = 100, dataset: str = "cifar1
         recs[:, lo] = labels
         if lb == 2:
             recs[:, 0] = labels // 5
-        # class-dependent mean so that a small model can learn something
-        base = (labels[:, None] * 23) % 256
-        recs[:, lb:] = np.clip(base + rng.integers(-40, 40, (n_per_file, 3072)), 0, 255).astype(np.uint8)
+        if learnable:
+            # hues evenly spaced around the colour wheel: distinct zero-mean channel patterns
+            hue = 2 * np.pi * np.arange(ncls) / ncls
+            palette = np.round(128 + 80 * np.cos(hue[:, None] - np.array([0, 2, 4]) * np.pi / 3)).astype(np.int64)
+            base = np.repeat(palette[labels], 1024, axis=1)  # CHW: each channel plane its own value
+            noise = rng.integers(-35, 36, (n_per_file, 3072))
+        else:  # class-dependent mean so that a small model can learn something
+            base = (labels[:, None] * 23) % 256
+            noise = rng.integers(-40, 40, (n_per_file, 3072))
+        recs[:, lb:] = np.clip(base + noise, 0, 255).astype(np.uint8)
         recs.tofile(os.path.join(d, name))
     return dirpath

@@ -157,81 +157,160 @@ def vgg_preprocess_np(img: np.ndarray, rh: int, rw: int, cy: int, cx: int, flip:
     return res - np.array(RGB_MEANS, dtype=np.float32)
 
 
+class _Shard:
+    """Record index of one TFRecord shard: the file is memory-mapped and only the 12-byte
+    record headers are walked (no payload read, no CRC) when the index is built; each record's
+    CRCs are checked when it is fetched."""
+
+    def __init__(self, path: str):
+        self.path = path
+        self._mm = None
+        self.offsets: Optional[np.ndarray] = None  # frame offsets (header start)
+        self.lengths: Optional[np.ndarray] = None
+
+    def _map(self):
+        if self._mm is None:
+            import mmap
+            with open(self.path, "rb") as f:
+                size = os.fstat(f.fileno()).st_size
+                self._mm = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ) if size else b""
+        return self._mm
+
+    def count(self) -> int:
+        if self.offsets is None:
+            import struct
+            mm = self._map()
+            offs, lens, pos, n = [], [], 0, len(mm)
+            while pos + 12 <= n:
+                (ln,) = struct.unpack_from("<Q", mm, pos)
+                if pos + 16 + ln > n:
+                    raise IOError(f"truncated TFRecord {self.path} at byte {pos}")
+                offs.append(pos)
+                lens.append(ln)
+                pos += 16 + ln
+            self.offsets = np.asarray(offs, dtype=np.int64)
+            self.lengths = np.asarray(lens, dtype=np.int64)
+        return len(self.offsets)
+
+    def record(self, i: int, check: bool = True) -> bytes:
+        self.count()
+        off, ln = int(self.offsets[i]), int(self.lengths[i])
+        frame = self._map()[off:off + 16 + ln]
+        if check:
+            from ..utils.tfrecord import scan
+            scan(frame, True)  # raises CorruptRecordError on a bad length / data CRC
+        return frame[12:12 + ln]
+
+
 class ImagenetLoader:
     """Background pipeline producing packed decoded batches:
-    (packed uint8 buffer, IMG_DESC array [B], int32 labels [B])."""
+    (packed uint8 buffer, IMG_DESC array [B], int32 labels [B]).
+
+    The record order is a pure function of (seed, rank, epoch): per-epoch file shuffle, then the
+    reference's 1500-deep example shuffle buffer (resnet_imagenet_main.py:165-173) run over
+    (shard, record) *indices*. A position is therefore just (epoch, records consumed in the
+    epoch), and resuming from a checkpoint skips that many indices without reading or decoding
+    any image. Crop/flip geometry of batch b comes from an RNG seeded with (seed, rank, b). Each
+    batch carries the position after it; `state()` reports the position after the last batch
+    handed out. With `pin=True` batches are packed straight into page-locked tensors.
+    """
 
     def __init__(self, data_dir: str, batch_size: int, is_training: bool, seed: int = 0, rank: int = 0,
-                 world: int = 1, num_threads: int = 8, prefetch: int = 3, num_epochs: Optional[int] = None):
-        self.files = filenames(is_training, data_dir)
+                 world: int = 1, num_threads: int = 8, prefetch: int = 3, num_epochs: Optional[int] = None,
+                 epoch: int = 0, cursor: int = 0, batch_index: int = 0, pin: bool = False, pin_device=None):
+        files = filenames(is_training, data_dir)
         if is_training and world > 1:
-            self.files = self.files[rank::world] or self.files
+            files = files[rank::world] or files
+        self.files = files
+        self.shards = [_Shard(f) for f in files]
         self.bs, self.train, self.seed, self.rank = batch_size, is_training, seed, rank
         self.num_epochs = num_epochs
+        self.pin, self.pin_device = pin, pin_device
+        self.epoch, self.cursor, self.batch_index = epoch, cursor, batch_index
         self.pool = ThreadPoolExecutor(max_workers=max(1, num_threads))
         self.q: "queue.Queue" = queue.Queue(maxsize=max(1, prefetch))
         self._stop = threading.Event()
         self._t = threading.Thread(target=self._run, daemon=True)
         self._t.start()
 
-    def _records(self):
-        rng = np.random.default_rng([self.seed, self.rank, 17])
-        epoch = 0
+    def epoch_order(self, epoch: int):
+        """Yields the (shard, record) indices of one epoch in training order."""
+        rng = np.random.default_rng([self.seed, self.rank, 17, epoch])
+        order = list(range(len(self.shards)))
+        if self.train:
+            rng.shuffle(order)
+        buf = []
+        for s in order:
+            for r in range(self.shards[s].count()):
+                if not self.train:
+                    yield s, r
+                    continue
+                buf.append((s, r))
+                if len(buf) >= SHUFFLE_BUFFER:
+                    j = int(rng.integers(0, len(buf)))
+                    buf[j], buf[-1] = buf[-1], buf[j]
+                    yield buf.pop()
+        while buf:
+            j = int(rng.integers(0, len(buf)))
+            buf[j], buf[-1] = buf[-1], buf[j]
+            yield buf.pop()
+
+    def _positions(self):
+        """(shard, record, epoch, cursor-after) from the resume position onwards."""
+        epoch, skip = self.epoch, self.cursor
         while not self._stop.is_set():
             if self.num_epochs is not None and epoch >= self.num_epochs:
                 return
-            files = list(self.files)
-            if self.train:
-                rng.shuffle(files)
-            buf = []
-            for fn in files:
-                for rec in read_records(fn):
-                    if self.train:
-                        buf.append(rec)
-                        if len(buf) >= SHUFFLE_BUFFER:
-                            j = int(rng.integers(0, len(buf)))
-                            buf[j], buf[-1] = buf[-1], buf[j]
-                            yield buf.pop()
-                    else:
-                        yield rec
-            while buf:
-                j = int(rng.integers(0, len(buf)))
-                buf[j], buf[-1] = buf[-1], buf[j]
-                yield buf.pop()
-            epoch += 1
+            n = 0
+            for s, r in self.epoch_order(epoch):
+                n += 1
+                if n <= skip:
+                    continue
+                yield s, r, epoch, n
+            epoch, skip = epoch + 1, 0
 
-    @staticmethod
-    def _decode(rec: bytes):
-        ex = parse_example(rec)
+    def _decode(self, pos):
+        ex = parse_example(self.shards[pos[0]].record(pos[1]))
         img = decode_image(ex["image/encoded"][0])
         label = int(ex.get("image/class/label", [-1])[0])
         return img, label
 
     def _run(self):
-        rng = np.random.default_rng([self.seed, self.rank, 99])
+        if self.pin and self.pin_device is not None:
+            import torch
+            torch.cuda.set_device(self.pin_device)
+        b = self.batch_index
         batch = []
         try:
-            for rec in self._records():
-                batch.append(rec)
+            for s, r, epoch, cursor in self._positions():
+                batch.append((s, r))
                 if len(batch) < self.bs:
                     continue
                 decoded = list(self.pool.map(self._decode, batch))
                 batch = []
-                sizes = [d[0].size for d in decoded]
-                packed = np.empty(sum(sizes), dtype=np.uint8)
+                rng = np.random.default_rng([self.seed, self.rank, 99, b])
+                total = sum(d[0].size for d in decoded)
+                if self.pin:
+                    import torch
+                    packed = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+                    flat = packed.numpy()
+                else:
+                    packed = flat = np.empty(total, dtype=np.uint8)
                 desc = np.zeros(self.bs, dtype=IMG_DESC)
                 labels = np.empty(self.bs, dtype=np.int32)
                 off = 0
                 for i, (img, lab) in enumerate(decoded):
                     h, w = img.shape[:2]
-                    packed[off:off + img.size] = img.reshape(-1)
+                    flat[off:off + img.size] = img.reshape(-1)
                     rh, rw, cy, cx, flip = draw_geometry(h, w, self.train, rng)
                     desc[i] = (off, h, w, rh, rw, cy, cx, flip, 0)
                     labels[i] = lab
                     off += img.size
+                b += 1
+                item = (packed, desc, labels, {"data_epoch": epoch, "data_cursor": cursor, "data_batch": b})
                 while not self._stop.is_set():
                     try:
-                        self.q.put((packed, desc, labels), timeout=0.1)
+                        self.q.put(item, timeout=0.1)
                         break
                     except queue.Full:
                         continue
@@ -247,7 +326,12 @@ class ImagenetLoader:
         item = self.q.get()
         if item is None:
             raise StopIteration
-        return item
+        packed, desc, labels, st = item
+        self.epoch, self.cursor, self.batch_index = st["data_epoch"], st["data_cursor"], st["data_batch"]
+        return packed, desc, labels
+
+    def state(self):
+        return {"data_epoch": self.epoch, "data_cursor": self.cursor, "data_batch": self.batch_index}
 
     def close(self):
         self._stop.set()

@@ -74,9 +74,10 @@ def evaluate(FLAGS, eval_batch_size: int = 100, max_evals: int = -1):
                         if not feeder.next():
                             break
                         ex.forward(train=False)
-                        total_loss += float(ex.loss_vec.double().sum())
-                        correct += int(ex.correct.sum())
-                        total += ex.N
+                        v = int(getattr(feeder, "valid", ex.N))  # wrapped padding of a final partial batch
+                        total_loss += float(ex.loss_vec[:v].double().sum())
+                        correct += int(ex.correct[:v].sum())
+                        total += v
                 finally:
                     feeder.close()
                 precision = correct / max(total, 1)

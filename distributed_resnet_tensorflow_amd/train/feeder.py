@@ -31,85 +31,126 @@ class SyntheticFeeder:
         pass
 
 
-class CifarFeeder:
-    def __init__(self, ex, loader: "cifar_data.CifarLoader", is_training: bool):
-        self.ex, self.loader, self.train = ex, loader, is_training
-        N = ex.N
-        dev = ex.device
-        self.gpu = dev.type == "cuda"
-        pin = self.gpu
-        self.h_img = torch.empty(N, 32, 32, 3, dtype=torch.uint8, pin_memory=pin)
-        self.h_lab = torch.empty(N, dtype=torch.int32, pin_memory=pin)
-        self.h_par = torch.empty(N, 3, dtype=torch.int32, pin_memory=pin)
-        self.d_img = torch.empty(N, 32, 32, 3, dtype=torch.uint8, device=dev)
-        self.d_par = torch.empty(N, 3, dtype=torch.int32, device=dev)
-        self.d_lab = torch.empty(N, dtype=torch.int32, device=dev)
-        self.copy_stream = torch.cuda.Stream(device=dev) if self.gpu else None
-        self._pending = None
-        self._prefetch()
+def _as_tensor(x):
+    return x if isinstance(x, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(x))
 
-    def _prefetch(self):
-        imgs, labels, params = next(self.loader)
+
+class _StagedFeeder:
+    """Common GPU staging: batch k+1 is copied host->device on a side stream while step k runs.
+
+    The loaders hand out a fresh page-locked buffer per batch (PyTorch's caching host
+    allocator keeps a block out of circulation until the async copies recorded on it complete),
+    so host-side writes can never race an in-flight DMA however far the host runs ahead of the
+    GPU (graph replay). The device-side staging buffers are reused: a copy into them waits for
+    the main stream's consumers of the previous batch (copy_stream.wait_stream).
+
+    `state()` is the loader position after the batch most recently handed to the executor (not
+    after the batch being prefetched), so a checkpoint resumes with the next unconsumed batch;
+    `valid` is that batch's number of real (non-wrapped) images.
+    """
+
+    def _init_staging(self, ex):
+        self.ex = ex
+        self.gpu = ex.device.type == "cuda"
+        self.copy_stream = torch.cuda.Stream(device=ex.device) if self.gpu else None
+        self._pending = None
+        self._pending_state, self._pending_valid = self.loader.state(), ex.N
+        self._state, self.valid = self.loader.state(), ex.N
+        self._exhausted = False
+
+    def _stage(self, pairs):
+        """pairs: [(device dst, host src)]; enqueues the copies on the copy stream."""
         if self.gpu:
-            # the previous batch's consumers (augment kernel) must be done with the staging tensors
             self.copy_stream.wait_stream(torch.cuda.current_stream(self.ex.device))
-            self.h_img.numpy()[...] = imgs
-            self.h_lab.numpy()[...] = labels
-            self.h_par.numpy()[...] = params
             with torch.cuda.stream(self.copy_stream):
-                self.d_img.copy_(self.h_img, non_blocking=True)
-                self.d_par.copy_(self.h_par, non_blocking=True)
-                self.d_lab.copy_(self.h_lab, non_blocking=True)
+                for dst, src in pairs:
+                    dst.copy_(_as_tensor(src), non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self.copy_stream)
             self._pending = ev
         else:
-            self.d_img.copy_(torch.from_numpy(imgs))
-            self.d_par.copy_(torch.from_numpy(params))
-            self.d_lab.copy_(torch.from_numpy(labels))
+            for dst, src in pairs:
+                dst.copy_(_as_tensor(src))
+
+    def _prefetch(self):
+        try:
+            item = next(self.loader)
+        except StopIteration:
+            self._exhausted = True
+            return
+        self._pending_state = self.loader.state()
+        self._pending_valid = int(getattr(self.loader, "valid", self.ex.N))
+        self._stage_item(item)
+
+    def _wait(self):
+        if self.gpu and self._pending is not None:
+            torch.cuda.current_stream(self.ex.device).wait_event(self._pending)
 
     def next(self):
-        if self.gpu:
-            torch.cuda.current_stream(self.ex.device).wait_event(self._pending)
-        self.ex.be.cifar_augment(self.d_img, self.d_par, self.ex.images, cifar_data.PAD)
-        self.ex.labels.copy_(self.d_lab)
+        if self._exhausted:
+            return False
+        self._wait()
+        self._consume()
+        self._state, self.valid = self._pending_state, self._pending_valid
         self._prefetch()
         return True
 
     def state(self):
-        return self.loader.state()
+        return dict(self._state)
 
     def close(self):
         self.loader.close()
 
 
-class ImagenetFeeder:
+class CifarFeeder(_StagedFeeder):
+    def __init__(self, ex, loader: "cifar_data.CifarLoader", is_training: bool):
+        self.loader, self.train = loader, is_training
+        N, dev = ex.N, ex.device
+        self.d_img = torch.empty(N, 32, 32, 3, dtype=torch.uint8, device=dev)
+        self.d_par = torch.empty(N, 3, dtype=torch.int32, device=dev)
+        self.d_lab = torch.empty(N, dtype=torch.int32, device=dev)
+        self._init_staging(ex)
+        self._prefetch()
+
+    def _stage_item(self, item):
+        imgs, labels, params = item
+        self._stage([(self.d_img, imgs), (self.d_par, params), (self.d_lab, labels)])
+
+    def _consume(self):
+        self.ex.be.cifar_augment(self.d_img, self.d_par, self.ex.images, cifar_data.PAD)
+        self.ex.labels.copy_(self.d_lab)
+
+
+class ImagenetFeeder(_StagedFeeder):
     def __init__(self, ex, loader, is_training: bool, max_bytes: int = 64 << 20):
         from ..data import imagenet as inet
         self.inet = inet
-        self.ex, self.loader = ex, loader
-        self.gpu = ex.device.type == "cuda"
+        self.loader = loader
         self.d_buf = torch.empty(max_bytes, dtype=torch.uint8, device=ex.device)
         self.d_desc = torch.empty(ex.N * inet.IMG_DESC.itemsize, dtype=torch.uint8, device=ex.device)
+        self.d_lab = torch.empty(ex.N, dtype=torch.int32, device=ex.device)
+        self.h_packed = None  # CPU path: the reference backend preprocesses from host memory
+        self.h_desc = None
+        self._init_staging(ex)
+        self._prefetch()
 
-    def next(self):
-        try:
-            packed, desc, labels = next(self.loader)
-        except StopIteration:
-            return False
+    def _stage_item(self, item):
+        packed, desc, labels = item
+        n = int(packed.numel() if isinstance(packed, torch.Tensor) else packed.size)
+        if not self.gpu:
+            self.h_packed, self.h_desc = packed, desc
+            self.d_lab.copy_(torch.from_numpy(labels))
+            return
+        if n > self.d_buf.numel():
+            # stream-ordered reallocation: the old buffer is released only after the main
+            # stream's last reader of it (the previous preprocess) is done
+            torch.cuda.current_stream(self.ex.device).synchronize()
+            self.d_buf = torch.empty(int(n * 1.25), dtype=torch.uint8, device=self.ex.device)
+        self._stage([(self.d_buf[:n], packed), (self.d_desc, desc.view(np.uint8)), (self.d_lab, labels)])
+
+    def _consume(self):
         if self.gpu:
-            if packed.size > self.d_buf.numel():
-                self.d_buf = torch.empty(int(packed.size * 1.25), dtype=torch.uint8, device=self.ex.device)
-            self.d_buf[:packed.size].copy_(torch.from_numpy(packed), non_blocking=False)
-            self.d_desc.copy_(torch.from_numpy(desc.view(np.uint8)))
             self.ex.be.vgg_preprocess(self.d_buf, self.d_desc, self.ex.images, self.inet.RGB_MEANS)
         else:
-            self.ex.be.vgg_preprocess(packed, desc, self.ex.images, self.inet.RGB_MEANS)
-        self.ex.labels.copy_(torch.from_numpy(labels))
-        return True
-
-    def state(self):
-        return {}
-
-    def close(self):
-        self.loader.close()
+            self.ex.be.vgg_preprocess(self.h_packed, self.h_desc, self.ex.images, self.inet.RGB_MEANS)
+        self.ex.labels.copy_(self.d_lab)

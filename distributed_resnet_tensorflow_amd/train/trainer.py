@@ -42,12 +42,16 @@ def apply_thread_flags(FLAGS):
 def model_spec_from_flags(FLAGS):
     ds = FLAGS.dataset
     model = FLAGS.model if FLAGS.model != "lrnet" else "resnet"
-    return build_spec(ds, FLAGS.resnet_size, model=model, width=FLAGS.width_multiplier)
+    # --width_multiplier only shapes --model=wide_resnet; --model=resnet is always the reference's
+    # ResNet-v2 (resnet_model.py:74, resnet_imagenet_main.py:266-272: 25,551,401 params at size 50)
+    width = FLAGS.width_multiplier if model == "wide_resnet" else 1
+    return build_spec(ds, FLAGS.resnet_size, model=model, width=width)
 
 
 def _meta(FLAGS, spec):
     return {"dataset": FLAGS.dataset, "resnet_size": FLAGS.resnet_size, "model": FLAGS.model,
-            "width_multiplier": FLAGS.width_multiplier, "num_classes": spec.num_classes,
+            "width_multiplier": FLAGS.width_multiplier if FLAGS.model == "wide_resnet" else 1,
+            "num_classes": spec.num_classes,
             "spec_name": spec.name}
 
 
@@ -55,19 +59,23 @@ def make_feeder(FLAGS, ex, cluster, is_training: bool, data_state=None, batch=No
     bs = batch or ex.N
     if FLAGS.synthetic_data:
         return SyntheticFeeder(ex, seed=FLAGS.seed + 101 * cluster.rank)
+    ds = data_state or {}
+    gpu = ex.device.type == "cuda"
+    pin = dict(pin=gpu, pin_device=ex.device if gpu else None)
     if FLAGS.dataset in ("cifar10", "cifar100"):
         path = FLAGS.train_data_path if is_training else FLAGS.eval_data_path
         recs = cifar_data.CifarRecords(cifar_data.get_filenames(is_training, path, FLAGS.dataset), FLAGS.dataset)
-        ds = data_state or {}
         loader = cifar_data.CifarLoader(recs, bs, is_training, seed=FLAGS.seed, rank=cluster.rank,
                                         world=cluster.world, epoch=int(ds.get("data_epoch", 0)),
-                                        cursor=int(ds.get("data_cursor", 0)))
+                                        cursor=int(ds.get("data_cursor", 0)), **pin)
         return CifarFeeder(ex, loader, is_training)
     from ..data import imagenet
     path = FLAGS.train_data_path if is_training else FLAGS.eval_data_path
     loader = imagenet.ImagenetLoader(path, bs, is_training, seed=FLAGS.seed, rank=cluster.rank, world=cluster.world,
                                      num_threads=max(2, FLAGS.num_workers * 4),
-                                     num_epochs=FLAGS.num_epochs if is_training else 1)
+                                     num_epochs=FLAGS.num_epochs if is_training else 1,
+                                     epoch=int(ds.get("data_epoch", 0)), cursor=int(ds.get("data_cursor", 0)),
+                                     batch_index=int(ds.get("data_batch", 0)), **pin)
     return ImagenetFeeder(ex, loader, is_training)
 
 

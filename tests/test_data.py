@@ -90,3 +90,94 @@ def test_imagenet_loader_batches(tmp_path):
     be.vgg_preprocess(packed, desc, out, imagenet.RGB_MEANS)
     assert torch.isfinite(out).all() and out[..., 3:].abs().max() == 0
     ld.close()
+
+
+def _drain(loader, n):
+    out = []
+    for _ in range(n):
+        b = next(loader)
+        out.append(tuple(np.array(x, copy=True) for x in b))
+    return out
+
+
+def test_cifar_loader_resume_is_exact(tmp_path):
+    """A loader restarted from the position recorded after batch k yields batch k+1 (same
+    images, labels and crop/flip draws), across an epoch boundary too."""
+    cifar.write_fake_cifar(str(tmp_path), 20)
+    rec = cifar.CifarRecords(cifar.get_filenames(True, str(tmp_path)))
+    ld = cifar.CifarLoader(rec, 16, True, seed=5)
+    ref, states = [], []
+    for _ in range(9):  # 100 records / 16 -> 6 batches per epoch: crosses into epoch 1
+        ref.append(tuple(np.array(x, copy=True) for x in next(ld)))
+        states.append(ld.state())
+    ld.close()
+    for k in (0, 4, 5, 7):
+        r = cifar.CifarLoader(rec, 16, True, seed=5, epoch=states[k]["data_epoch"], cursor=states[k]["data_cursor"])
+        got = _drain(r, 1)[0]
+        r.close()
+        for a, b in zip(got, ref[k + 1]):
+            np.testing.assert_array_equal(a, b)
+
+
+def test_cifar_eval_partial_batch_valid_count(tmp_path):
+    cifar.write_fake_cifar(str(tmp_path), 50)
+    rec = cifar.CifarRecords(cifar.get_filenames(False, str(tmp_path)))
+    ld = cifar.CifarLoader(rec, 20, False)
+    valids = []
+    for _ in range(3):
+        next(ld)
+        valids.append(ld.valid)
+    ld.close()
+    assert valids == [20, 20, 10]  # the wrapped tail of the last batch is not counted
+
+
+def test_cifar_feeder_state_is_consumed_batch(tmp_path):
+    """CPU feeder: state() after next() is the position after the batch now in the executor
+    (not after the prefetched one), and the labels in the executor are that batch's."""
+    from distributed_resnet_tensorflow_amd.models.spec import build_spec
+    from distributed_resnet_tensorflow_amd.runtime.executor import Executor
+    from distributed_resnet_tensorflow_amd.train.feeder import CifarFeeder
+    cifar.write_fake_cifar(str(tmp_path), 20)
+    rec = cifar.CifarRecords(cifar.get_filenames(True, str(tmp_path)))
+    ref_ld = cifar.CifarLoader(rec, 8, True, seed=2)
+    ref = _drain(ref_ld, 4)
+    ref_ld.close()
+    ex = Executor(build_spec("cifar10", 8), 8, RefBackend(), "cpu")
+    f = CifarFeeder(ex, cifar.CifarLoader(rec, 8, True, seed=2), True)
+    for k in range(4):
+        assert f.next()
+        np.testing.assert_array_equal(ex.labels.numpy(), ref[k][1])
+        assert f.state() == {"data_epoch": 0, "data_cursor": 8 * (k + 1)}
+    f.close()
+
+
+def test_imagenet_loader_resume_is_exact(tmp_path):
+    """(epoch, records consumed, batch index) is a complete position: a restarted loader
+    continues with the same records and the same crop/flip draws, across epochs."""
+    imagenet.write_fake_imagenet(str(tmp_path), shards=3, per_shard=4)
+    ld = imagenet.ImagenetLoader(str(tmp_path), 5, True, seed=1, num_threads=2)
+    ref, states = [], []
+    for _ in range(5):  # 12 records / epoch, 5 per batch: batches straddle epochs
+        p, d, l = next(ld)
+        ref.append((np.array(p, copy=True), d.copy(), l.copy()))
+        states.append(ld.state())
+    ld.close()
+    assert states[1]["data_epoch"] == 0 and states[2]["data_epoch"] == 1
+    for k in (0, 1, 2, 3):
+        st = states[k]
+        r = imagenet.ImagenetLoader(str(tmp_path), 5, True, seed=1, num_threads=2, epoch=st["data_epoch"],
+                                    cursor=st["data_cursor"], batch_index=st["data_batch"])
+        p, d, l = next(r)
+        r.close()
+        np.testing.assert_array_equal(l, ref[k + 1][2])
+        np.testing.assert_array_equal(d, ref[k + 1][1])
+        np.testing.assert_array_equal(np.asarray(p), ref[k + 1][0])
+
+
+def test_imagenet_epoch_order_is_a_permutation(tmp_path):
+    imagenet.write_fake_imagenet(str(tmp_path), shards=3, per_shard=7)
+    ld = imagenet.ImagenetLoader(str(tmp_path), 4, True, seed=3, num_threads=1, num_epochs=1)
+    o0, o1 = list(ld.epoch_order(0)), list(ld.epoch_order(1))
+    ld.close()
+    assert sorted(o0) == sorted(o1) == [(s, r) for s in range(3) for r in range(7)]
+    assert o0 != o1

@@ -46,3 +46,15 @@ def test_precision_flag_validation():
     assert make_backend("cpu", "bf16").name == "ref"      # CPU: always the fp32 reference backend
     with _pt.raises(ValueError):
         make_backend("cpu", "fp16")
+
+
+def test_imagenet_entry_defaults_build_resnet50_v2():
+    """resnet_imagenet_main.py / resnet_imagenet_eval.py with default flags build the reference's
+    ResNet-v2-50 (resnet_model.py:74): --width_multiplier only applies to --model=wide_resnet."""
+    from distributed_resnet_tensorflow_amd.cli import entry_flags
+    from distributed_resnet_tensorflow_amd.train.trainer import model_spec_from_flags
+    for entry in ("imagenet_main", "imagenet_eval_main"):
+        spec = model_spec_from_flags(entry_flags(entry, []))
+        assert spec.num_params() == 25_551_401, (entry, spec.name)
+    F = entry_flags("imagenet_main", ["--model=wide_resnet"])
+    assert model_spec_from_flags(F).num_params() == 68_877_609
