@@ -88,6 +88,18 @@ class CifarRecords:
         images[:] = recs[:, self.label_bytes:].reshape(-1, DEPTH, HEIGHT, WIDTH).transpose(0, 2, 3, 1)
 
 
+def _device_index(dev):
+    """Integer GPU index of `dev` (None, 'cuda', 'cuda:1', torch.device, int); resolved on the
+    constructing (main) thread so a loader thread can select the same device."""
+    import torch
+    if dev is None:
+        return torch.cuda.current_device()
+    if isinstance(dev, int):
+        return dev
+    d = torch.device(dev)
+    return d.index if d.index is not None else torch.cuda.current_device()
+
+
 def _host_array(shape, dtype, pin: bool):
     """(tensor-or-array, numpy view) of a fresh host buffer; page-locked when `pin`."""
     if not pin:
@@ -115,7 +127,8 @@ class CifarLoader:
                  world: int = 1, prefetch: int = 4, epoch: int = 0, cursor: int = 0, pin: bool = False,
                  pin_device=None):
         self.rec = records
-        self.pin, self.pin_device = pin, pin_device
+        self.pin, self.pin_device = pin, _device_index(pin_device) if pin else None
+        self._error: Optional[BaseException] = None
         self.valid = batch_size
         self.bs = batch_size
         self.train = is_training
@@ -135,6 +148,13 @@ class CifarLoader:
         return p[self.rank * per:(self.rank + 1) * per]
 
     def _run(self):
+        try:
+            self._produce()
+        except BaseException as e:  # surfaces in the consumer's next() instead of a silent hang
+            self._error = e
+            self.q.put(None)
+
+    def _produce(self):
         if self.pin and self.pin_device is not None:
             import torch
             torch.cuda.set_device(self.pin_device)  # page-locked allocations in this rank's context
@@ -179,7 +199,10 @@ class CifarLoader:
         return self
 
     def __next__(self):
-        imgs, labels, params, epoch, cursor, valid = self.q.get()
+        item = self.q.get()
+        if item is None:
+            raise RuntimeError("CIFAR loader thread failed") from self._error
+        imgs, labels, params, epoch, cursor, valid = item
         self.epoch, self.cursor, self.valid = epoch, cursor, valid
         return imgs, labels, params
 

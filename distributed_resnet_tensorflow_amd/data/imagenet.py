@@ -225,7 +225,9 @@ class ImagenetLoader:
         self.shards = [_Shard(f) for f in files]
         self.bs, self.train, self.seed, self.rank = batch_size, is_training, seed, rank
         self.num_epochs = num_epochs
-        self.pin, self.pin_device = pin, pin_device
+        from .cifar import _device_index
+        self.pin, self.pin_device = pin, _device_index(pin_device) if pin else None
+        self._error: Optional[BaseException] = None
         self.epoch, self.cursor, self.batch_index = epoch, cursor, batch_index
         self.pool = ThreadPoolExecutor(max_workers=max(1, num_threads))
         self.q: "queue.Queue" = queue.Queue(maxsize=max(1, prefetch))
@@ -276,12 +278,12 @@ class ImagenetLoader:
         return img, label
 
     def _run(self):
-        if self.pin and self.pin_device is not None:
-            import torch
-            torch.cuda.set_device(self.pin_device)
         b = self.batch_index
         batch = []
         try:
+            if self.pin and self.pin_device is not None:
+                import torch
+                torch.cuda.set_device(self.pin_device)
             for s, r, epoch, cursor in self._positions():
                 batch.append((s, r))
                 if len(batch) < self.bs:
@@ -316,6 +318,8 @@ class ImagenetLoader:
                         continue
                 if self._stop.is_set():
                     return
+        except BaseException as e:  # surfaces in the consumer's next() instead of a silent stop
+            self._error = e
         finally:
             self.q.put(None)
 
@@ -325,6 +329,8 @@ class ImagenetLoader:
     def __next__(self):
         item = self.q.get()
         if item is None:
+            if self._error is not None:
+                raise RuntimeError("ImageNet loader thread failed") from self._error
             raise StopIteration
         packed, desc, labels, st = item
         self.epoch, self.cursor, self.batch_index = st["data_epoch"], st["data_cursor"], st["data_batch"]

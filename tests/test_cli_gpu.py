@@ -38,9 +38,9 @@ def test_cifar_gpu_train_checkpoint_eval_converges(tmp_path):
     write_fake_cifar(data, 1000, learnable=True)
     ck, ev = str(tmp_path / "ck"), str(tmp_path / "ev")
     out = run(["resnet_cifar_main.py", "--num_gpus=1", f"--train_data_path={data}", f"--log_root={ck}",
-               "--resnet_size=8", "--batch_size=128", "--train_steps=150", "--log_every_n_steps=50"])
-    assert "global step 150" in out, out[-2000:]
-    assert os.path.exists(os.path.join(ck, "model.ckpt-150.index"))
+               "--resnet_size=8", "--batch_size=128", "--train_steps=2000", "--log_every_n_steps=50"])
+    assert "global step 2000" in out, out[-2000:]
+    assert os.path.exists(os.path.join(ck, "model.ckpt-2000.index"))
     out = run(["resnet_cifar_eval.py", "--mode=eval", "--eval_once=True", "--num_gpus=1",
                f"--eval_data_path={data}/cifar-10-batches-bin/test_batch*", f"--log_root={ck}", f"--eval_dir={ev}",
                "--resnet_size=8", "--eval_batch_count=10"])
@@ -48,7 +48,7 @@ def test_cifar_gpu_train_checkpoint_eval_converges(tmp_path):
     assert m, out[-2000:]
     assert float(m[-1]) > 0.9, out[-2000:]
     best = json.load(open(os.path.join(ev, "best_precision.json")))
-    assert best["step"] == 150 and best["best_precision"] > 0.9
+    assert best["step"] == 2000 and best["best_precision"] > 0.9
 
 
 @pytest.mark.timeout(600)

@@ -113,20 +113,22 @@ def test_cifar_feeder_host_ahead_keeps_batches(tmp_path):
     ex = Executor(cifar_resnet_v2(8), N, HipBackend(), "cuda")
     f = CifarFeeder(ex, cifar.CifarLoader(rec, N, True, seed=4, pin=True, pin_device=ex.device), True)
     hist_lab = torch.empty(steps, N, dtype=torch.int32, device="cuda")
-    hist_img = torch.empty(steps, N, 32, 32, 3, dtype=torch.uint8, device="cuda")
-    hist_par = torch.empty(steps, N, 3, dtype=torch.int32, device="cuda")
+    hist_img = torch.empty(steps, N, 32, 32, 3, dtype=torch.bfloat16, device="cuda")
     for k in range(steps):
         assert f.next()
+        # what the step consumes: the augmented batch in the executor's input buffers
         hist_lab[k].copy_(ex.labels)
-        hist_img[k].copy_(f.d_img)  # the device staging buffer the augment kernel just read
-        hist_par[k].copy_(f.d_par)
-        _busy()   # the host enqueues the next prefetch long before this finishes
+        hist_img[k].copy_(ex.images[..., :3])
+        _busy()   # the host enqueues the next prefetches long before this finishes
     torch.cuda.synchronize()
     f.close()
+    rb = RefBackend()
     for k in range(steps):
         np.testing.assert_array_equal(hist_lab[k].cpu().numpy(), ref[k][1], err_msg=f"labels of batch {k}")
-        np.testing.assert_array_equal(hist_img[k].cpu().numpy(), ref[k][0], err_msg=f"images of batch {k}")
-        np.testing.assert_array_equal(hist_par[k].cpu().numpy(), ref[k][2], err_msg=f"aug params of batch {k}")
+        want = torch.zeros(N, 32, 32, 8)
+        rb.cifar_augment(torch.from_numpy(ref[k][0]), torch.from_numpy(ref[k][2]), want, cifar.PAD)
+        err = (hist_img[k].float().cpu() - want[..., :3]).abs().max().item()
+        assert err < 0.03, (k, err)  # bf16 rounding of standardised pixels; a wrong batch is O(1)
 
 
 def test_imagenet_feeder_gpu_vs_cpu_and_resume(tmp_path):
