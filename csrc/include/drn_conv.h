@@ -18,6 +18,100 @@ __device__ __forceinline__ uint32_t drn_fdiv(uint32_t n, const DrnFastDiv& f) {
 }
 #endif
 
+// BatchNorm finalize performed by the CONSUMER of the statistics (no separate finalize launch).
+// Every workgroup of the consuming kernel derives the per-channel parameters it needs from the
+// [G][2][C] statistics replicas in its prologue; the workgroup with blockIdx.x == 0 of the
+// launch flagged `publish` also writes them to global memory for later kernels (and updates the
+// moving averages / writes the parameter gradients). All consumers use the same device function,
+// so locally derived and published values are bitwise identical.
+//   forward : stats = (sum x, sum x^2); outputs scale/shift/mean/invstd (+ run_mean/run_var)
+//   backward: stats = (sum g, sum g*xhat); inputs invstd; outputs dgamma = sum g*xhat,
+//             dbeta = sum g
+struct DrnBnFin {
+  const float* stats;
+  const float* gamma;
+  const float* beta;
+  float* run_mean;
+  float* run_var;
+  float* scale;
+  float* shift;
+  float* mean;
+  float* invstd;
+  float* dgamma;
+  float* dbeta;
+  int32_t G, C;
+  float count, eps, momentum;
+  int32_t publish;
+};
+
+#if defined(__HIPCC__)
+// standalone forward finalize of a DrnBnFin (bn.hip; the fallback when no consumer kernel can
+// finalize in its prologue)
+extern "C" int drn_bn_fin_fwd_launch(const DrnBnFin* f, hipStream_t s);
+
+// Sum of the G (<= DRN_BN_FIN_GMAX) replicas of channel c: every load is issued unconditionally
+// (index clamped, the surplus masked after the load) so all 2*GMAX loads are in flight together
+// instead of one dependent round trip per replica of a runtime-length loop.
+#define DRN_BN_FIN_GMAX 8
+__device__ __forceinline__ void drn_bn_fin_sums(const DrnBnFin& f, int c, float& s, float& q) {
+  float sv[DRN_BN_FIN_GMAX], qv[DRN_BN_FIN_GMAX];
+#pragma unroll
+  for (int r = 0; r < DRN_BN_FIN_GMAX; ++r) {
+    const int rr = r < f.G ? r : f.G - 1;
+    sv[r] = f.stats[(size_t)(2 * rr) * f.C + c];
+    qv[r] = f.stats[(size_t)(2 * rr + 1) * f.C + c];
+  }
+  s = 0.f;
+  q = 0.f;
+#pragma unroll
+  for (int r = 0; r < DRN_BN_FIN_GMAX; ++r) {
+    s += r < f.G ? sv[r] : 0.f;
+    q += r < f.G ? qv[r] : 0.f;
+  }
+}
+
+// forward finalize of channel c (fp32 from the fp32 sums: short dependent chain, it sits in
+// the prologue of every consuming workgroup; TF fused-BN moving averages)
+__device__ __forceinline__ void drn_bn_fin_fwd(const DrnBnFin& f, int c, bool pub, float& sc, float& sh) {
+  float s, q;
+  drn_bn_fin_sums(f, c, s, q);
+  const float inv_n = 1.f / f.count;
+  const float mean = s * inv_n;
+  const float var = fmaxf(fmaf(-mean, mean, q * inv_n), 0.f);
+  const float invstd = 1.f / sqrtf(var + f.eps);
+  sc = f.gamma[c] * invstd;
+  sh = fmaf(-mean, sc, f.beta[c]);
+  if (pub) {
+    f.scale[c] = sc;
+    f.shift[c] = sh;
+    f.mean[c] = mean;
+    f.invstd[c] = invstd;
+    if (f.run_mean != nullptr) {
+      const float n = f.count;
+      const float unbiased = n > 1.f ? var * (n / (n - 1.f)) : var;
+      f.run_mean[c] = f.momentum * f.run_mean[c] + (1.f - f.momentum) * mean;
+      f.run_var[c] = f.momentum * f.run_var[c] + (1.f - f.momentum) * unbiased;
+    }
+  }
+}
+
+// backward finalize of channel c: dx = k1 * (g - k2 - xhat * k3) with k1 = gamma * invstd,
+// k2 = mean(g), k3 = mean(g * xhat); returned folded as dx = A*g + B*x + D
+__device__ __forceinline__ void drn_bn_fin_bwd(const DrnBnFin& f, int c, bool pub, float& A, float& B, float& D) {
+  float sg, sgx;
+  drn_bn_fin_sums(f, c, sg, sgx);
+  const float is = f.invstd[c], mu = f.mean[c];
+  const float k1 = f.gamma[c] * is, k2 = sg / f.count, k3 = sgx / f.count;
+  A = k1;
+  B = -k1 * k3 * is;
+  D = -k1 * k2 + k1 * k3 * is * mu;
+  if (pub) {
+    f.dbeta[c] = sg;
+    f.dgamma[c] = sgx;
+  }
+}
+#endif
+
 // y[N][P][Q][K] = conv(x[N][H][W][C], w[K][R][S][C])  (NHWC / KRSC, bf16, fp32 accumulate)
 //
 // The same kernel runs the data-gradient of a convolution as a forward convolution of dY with
@@ -81,6 +175,10 @@ struct DrnConvFwdArgs {
   float* fin_coef;
   // pixel-index decode m -> (n, p, q): divisors P*Q and Q (filled by the host)
   DrnFastDiv fd_pq, fd_q;
+  // Optional consumer-side finalize of the INPUT BatchNorm (LDS-DMA kernels with the fused
+  // prologue): when in_fin.stats is set the prologue derives scale/shift from the statistics
+  // instead of reading in_scale/in_shift (see DrnBnFin).
+  DrnBnFin in_fin;
 };
 
 // dW[K][R][S][C] (+)= sum_{n,p,q} dy[n,p,q,k] * x[n, p*st-pad+r, q*st-pad+s, c]

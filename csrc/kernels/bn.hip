@@ -18,6 +18,7 @@
 // fp32 atomics make the statistics order-nondeterministic in the last bits (like cuDNN's).
 // Every kernel reads/writes 16-byte vectors (8 channels) per lane.
 #include "drn_common.h"
+#include "drn_conv.h"
 #include <stdlib.h>
 
 namespace drn {
@@ -437,6 +438,155 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_stats_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Consumer-side finalize (DrnBnFin, drn_conv.h): the streaming apply kernels derive the BN
+// parameters of ALL channels into LDS in their prologue (every workgroup, from the [G][2][C]
+// statistics replicas; workgroup 0 publishes them), so no separate finalize launch sits on the
+// critical path between the statistics producer and the apply.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bn_fin_fwd_kernel(DrnBnFin f) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= f.C) return;
+  float sc, sh;
+  drn_bn_fin_fwd(f, c, true, sc, sh);
+}
+
+// y = relu(x * scale + shift) with scale/shift finalized in the prologue. CV = C/8 is a power
+// of two <= 256, so a 256-thread block covers every 8-channel group and each thread keeps its
+// group fixed across the grid-stride loop (two 16-byte vectors in flight per iteration).
+__global__ __launch_bounds__(256) void bn_apply_fin_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                           DrnBnFin f, int64_t nvec, int CV, int relu) {
+  extern __shared__ __attribute__((aligned(16))) float lsm[];  // [2][C]
+  const int C = CV * 8;
+  const bool pub = f.publish && blockIdx.x == 0;
+  for (int c = threadIdx.x; c < C; c += 256) drn_bn_fin_fwd(f, c, pub, lsm[c], lsm[C + c]);
+  __syncthreads();
+  const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int c = (int)(i0 & (CV - 1)) * 8;
+  float sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = lsm[c + j];
+    sh[j] = lsm[C + c + j];
+  }
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const uint4* xv = reinterpret_cast<const uint4*>(x);
+  uint4* yv = reinterpret_cast<uint4*>(y);
+  int64_t i = i0;
+  for (; i + stride < nvec; i += 2 * stride) {
+    const uint4 v0 = xv[i], v1 = xv[i + stride];
+    float f0[8], f1[8];
+    unpack8(v0, f0);
+    unpack8(v1, f1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f0[j] = f0[j] * sc[j] + sh[j];
+      f1[j] = f1[j] * sc[j] + sh[j];
+      if (relu) {
+        f0[j] = fmaxf(f0[j], 0.f);
+        f1[j] = fmaxf(f1[j], 0.f);
+      }
+    }
+    yv[i] = pack8(f0);
+    yv[i + stride] = pack8(f1);
+  }
+  if (i < nvec) {
+    float f0[8];
+    unpack8(xv[i], f0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      f0[j] = f0[j] * sc[j] + sh[j];
+      if (relu) f0[j] = fmaxf(f0[j], 0.f);
+    }
+    yv[i] = pack8(f0);
+  }
+}
+
+// dx = A*g + B*x + D (+ add), g = dy masked by the forward ReLU (relu=1) or already masked
+// (relu=0: the producing data-gradient conv masked it in its epilogue); A/B/D of every channel
+// finalized in the prologue from the backward sums, workgroup 0 of a publishing launch writes
+// dgamma/dbeta. scale/shift (for the mask) and mean/invstd are the forward's published values.
+template <bool ADD>
+__device__ __forceinline__ void bn_bwd_fin_vec(const uint4& xv, float* fd, const uint4& av, const float* A,
+                                               const float* B, const float* D, const float* sc, const float* sh,
+                                               int relu) {
+  float fx[8], fa[8];
+  unpack8(xv, fx);
+  if constexpr (ADD) unpack8(av, fa);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float g = (relu && fx[j] * sc[j] + sh[j] <= 0.f) ? 0.f : fd[j];
+    float v = A[j] * g + B[j] * fx[j] + D[j];
+    if constexpr (ADD) v += fa[j];
+    fd[j] = v;
+  }
+}
+
+template <bool ADD>
+__global__ __launch_bounds__(256) void bn_bwd_apply_fin_kernel(DySrc src, const bf16_t* __restrict__ x,
+                                                               const float* __restrict__ scale,
+                                                               const float* __restrict__ shift, DrnBnFin f,
+                                                               const bf16_t* __restrict__ add, bf16_t* __restrict__ dx,
+                                                               int64_t nvec, int C, int relu) {
+  extern __shared__ __attribute__((aligned(16))) float lsm[];  // [3][C]
+  const bool pub = f.publish && blockIdx.x == 0;
+  for (int c = threadIdx.x; c < C; c += 256) drn_bn_fin_bwd(f, c, pub, lsm[c], lsm[C + c], lsm[2 * C + c]);
+  __syncthreads();
+  const int CV = C / 8;
+  const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int c = (int)(i0 & (CV - 1)) * 8;
+  const int cv_shift = __ffs(CV) - 1;
+  float A[8], B[8], D[8], sc[8], sh[8];
+  load8f(scale + c, sc);
+  load8f(shift + c, sh);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    A[j] = lsm[c + j];
+    B[j] = lsm[C + c + j];
+    D[j] = lsm[2 * C + c + j];
+  }
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const uint4* xv = reinterpret_cast<const uint4*>(x);
+  const uint4* av = reinterpret_cast<const uint4*>(add);
+  uint4* dv = reinterpret_cast<uint4*>(dx);
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  int64_t i = i0;
+  for (; i + stride < nvec; i += 2 * stride) {
+    float fd0[8], fd1[8];
+    const uint4 x0 = xv[i], x1 = xv[i + stride];
+    const uint4 a0 = ADD ? av[i] : z, a1 = ADD ? av[i + stride] : z;
+    src.load_vec(i, cv_shift, C, c, fd0);
+    src.load_vec(i + stride, cv_shift, C, c, fd1);
+    bn_bwd_fin_vec<ADD>(x0, fd0, a0, A, B, D, sc, sh, relu);
+    bn_bwd_fin_vec<ADD>(x1, fd1, a1, A, B, D, sc, sh, relu);
+    dv[i] = pack8(fd0);
+    dv[i + stride] = pack8(fd1);
+  }
+  if (i < nvec) {
+    float fd0[8];
+    const uint4 x0 = xv[i];
+    const uint4 a0 = ADD ? av[i] : z;
+    src.load_vec(i, cv_shift, C, c, fd0);
+    bn_bwd_fin_vec<ADD>(x0, fd0, a0, A, B, D, sc, sh, relu);
+    dv[i] = pack8(fd0);
+  }
+}
+
+// grid of the finalizing apply kernels: every workgroup re-derives the parameters of all C
+// channels (2*G*C + ~4*C floats from L2), so the grid is capped lower than the plain apply's
+static inline int grid_for_fin(int64_t nvec) {
+  static int cap = 0;
+  if (cap == 0) {
+    const char* e = getenv("DRN_BN_FIN_GRID");
+    cap = e ? atoi(e) : 2048;
+    if (cap < 1) cap = 2048;
+  }
+  int64_t b = (nvec + 511) / 512;  // >= 2 vectors per thread
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
 static int g_apply_grid_cap = 0;
 static inline int grid_for(int64_t nvec) {
   if (g_apply_grid_cap == 0) {
@@ -531,6 +681,51 @@ DRN_API int drn_bn_finalize_bwd(float* part, int G, int C, float count, const fl
                      invstd, dgamma, dbeta, coef);
   return (int)hipGetLastError();
 }
+
+static bool fin_ok(const DrnBnFin* f, int C) {
+  return f != nullptr && f->stats != nullptr && f->G >= 1 && f->G <= DRN_BN_FIN_GMAX && f->C == C &&
+         f->count > 0.f && f->gamma != nullptr;
+}
+
+DRN_API int drn_bn_fin_fwd_launch(const DrnBnFin* f, hipStream_t s) {
+  if (!fin_ok(f, f ? f->C : 0) || f->beta == nullptr || f->scale == nullptr || f->shift == nullptr ||
+      f->mean == nullptr || f->invstd == nullptr)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(drn::bn_fin_fwd_kernel, dim3((f->C + 255) / 256), dim3(256), 0, s, *f);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_bn_apply_fin(const void* x, void* y, const DrnBnFin* f, int64_t M, int C, int relu, hipStream_t s) {
+  if (C % 8 || !pow2(C / 8) || C / 8 > 256 || !fin_ok(f, C) || f->beta == nullptr ||
+      (f->publish && (f->scale == nullptr || f->shift == nullptr || f->mean == nullptr || f->invstd == nullptr)))
+    return (int)hipErrorInvalidValue;
+  const int64_t nvec = M * (C / 8);
+  hipLaunchKernelGGL(drn::bn_apply_fin_kernel, dim3(drn::grid_for_fin(nvec)), dim3(256), 2 * C * sizeof(float), s,
+                     (const bf16_t*)x, (bf16_t*)y, *f, nvec, C / 8, relu);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_bn_bwd_apply_fin(const void* dy, const float* dpool, int pool_hw, const void* x, const float* scale,
+                                 const float* shift, const DrnBnFin* f, const void* add, void* dx, int64_t M, int C,
+                                 int relu, hipStream_t s) {
+  if (C % 8 || !pow2(C / 8) || C / 8 > 256 || !fin_ok(f, C) || f->mean == nullptr || f->invstd == nullptr ||
+      (f->publish && (f->dgamma == nullptr || f->dbeta == nullptr)))
+    return (int)hipErrorInvalidValue;
+  const int64_t nvec = M * (C / 8);
+  drn::DySrc src{(const bf16_t*)dy, dpool, pool_hw};
+  if (add != nullptr)
+    hipLaunchKernelGGL(drn::bn_bwd_apply_fin_kernel<true>, dim3(drn::grid_for_fin(nvec)), dim3(256),
+                       3 * C * sizeof(float), s, src, (const bf16_t*)x, scale, shift, *f, (const bf16_t*)add,
+                       (bf16_t*)dx, nvec, C, relu);
+  else
+    hipLaunchKernelGGL(drn::bn_bwd_apply_fin_kernel<false>, dim3(drn::grid_for_fin(nvec)), dim3(256),
+                       3 * C * sizeof(float), s, src, (const bf16_t*)x, scale, shift, *f, (const bf16_t*)add,
+                       (bf16_t*)dx, nvec, C, relu);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_bn_fin_size() { return (int)sizeof(DrnBnFin); }
+DRN_API int drn_conv_args_size() { return (int)sizeof(DrnConvFwdArgs); }
 
 DRN_API int drn_bn_bwd_apply(const void* dy, const float* dpool, int pool_hw, const void* x, const float* scale,
                              const float* shift, const float* mean, const float* invstd, const float* coef,

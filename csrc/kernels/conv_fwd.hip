@@ -22,6 +22,7 @@
 // the NEXT BatchNorm's batch statistics.
 #include "drn_common.h"
 #include "drn_conv.h"
+#include <stdlib.h>
 
 namespace drn {
 
@@ -652,15 +653,9 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   const int swz = glds_swz<BK>(fr);  // fragment row groups are 16-aligned: the swizzle bits are fr's
 
   const int T = SROW ? a.R : Ktot / BK;
-  // fused-BN operands: [scale C][shift C] fp32 behind the stages (before any LDS-DMA is issued)
+  // fused-BN operands: [scale C][shift C] fp32 behind the stages, written AFTER the first
+  // pipeline stages are issued (their LDS-DMA latency covers the parameter loads / finalize)
   float* const ssl = reinterpret_cast<float*>(smem + NS * STAGE);
-  if constexpr (PRO) {
-    for (int c = tid * 4; c < C; c += NT * 4) {
-      *reinterpret_cast<float4*>(ssl + c) = *reinterpret_cast<const float4*>(a.in_scale + c);
-      *reinterpret_cast<float4*>(ssl + C + c) = *reinterpret_cast<const float4*>(a.in_shift + c);
-    }
-    __syncthreads();
-  }
   // the lane's logical 16-byte chunk of the B rows it loads: identical for every piece i
   // (RPG * NW rows apart leave the swizzle bits unchanged)
   static_assert((RPG * NW) % 16 == 0, "piece stride must preserve the swizzle bits");
@@ -671,6 +666,20 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
 #pragma unroll
   for (int s = 0; s < D; ++s)
     if (s < T) issue(s);
+  if constexpr (PRO) {
+    if (a.in_fin.stats != nullptr) {
+      // consumer-side BN finalize: scale/shift straight from the statistics replicas (the
+      // first workgroup of the publishing launch also writes them out for later kernels)
+      const bool pub = a.in_fin.publish && blockIdx.x == 0;
+      for (int c = tid; c < C; c += NT) drn_bn_fin_fwd(a.in_fin, c, pub, ssl[c], ssl[C + c]);
+    } else {
+      for (int c = tid * 4; c < C; c += NT * 4) {
+        *reinterpret_cast<float4*>(ssl + c) = *reinterpret_cast<const float4*>(a.in_scale + c);
+        *reinterpret_cast<float4*>(ssl + C + c) = *reinterpret_cast<const float4*>(a.in_shift + c);
+      }
+    }
+    __syncthreads();
+  }
 
   for (int t = 0; t < T; ++t) {
     // retire stage t: the stages issued after it (up to D-1) may stay in flight
@@ -737,6 +746,16 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   conv_epilogue<BP, BC, WP, WC, MI, MJ, NT, PF>(a, smem, acc, wp, wc, m0, c0, M, epre);
 }
 
+// largest grid that finalizes its input BatchNorm in the prologue (DRN_CFIN_MAX_BLOCKS)
+static int cfin_max_blocks() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DRN_CFIN_MAX_BLOCKS");
+    v = e ? atoi(e) : 2048;
+  }
+  return v;
+}
+
 template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF, int BK, bool PRO, bool SROW = false>
 static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
   constexpr int LDS0 = NS * (BC + BP) * BK * 2;
@@ -753,6 +772,18 @@ static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t 
   const int tiles_p = (M + BP - 1) / BP;
   const int tiles_c = (a->K + BC - 1) / BC;
   a->tiles_p = tiles_p;
+  if (PRO && a->in_fin.stats != nullptr && tiles_p * tiles_c > cfin_max_blocks()) {
+    // a large grid pays the in-prologue finalize once per workgroup wave: measured slower than
+    // one separate finalize launch (ResNet-50 stage 1, 12544 workgroups: +11 us vs ~6 us)
+    if (a->in_fin.publish) {
+      const int rc = drn_bn_fin_fwd_launch(&a->in_fin, stream);
+      if (rc) return rc;
+    }
+    DrnConvFwdArgs b = *a;
+    b.in_fin.stats = nullptr;
+    hipLaunchKernelGGL(kern, dim3(tiles_p * tiles_c), dim3(NW * 64), LDS, stream, b, zero);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(kern, dim3(tiles_p * tiles_c), dim3(NW * 64), LDS, stream, *a, zero);
   return (int)hipGetLastError();
 }
@@ -885,11 +916,25 @@ DRN_API int drn_conv_glds_ok(const DrnConvFwdArgs* a) {
 }
 
 // Dispatch on a->cfg; zero = >= 16 bytes of device zeros (the LDS-DMA loader's padding source).
+// A consumer-side BN finalize (in_fin) runs only on the LDS-DMA path; on the register-staged
+// kernel the finalize is a separate launch ahead of the conv (drn_bn_finalize semantics).
 DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
   if ((a->C % 8) != 0 || (a->K % 8) != 0) return (int)hipErrorInvalidValue;
   if (a->fin_cnt != nullptr && (a->stats == nullptr || a->K > 64 * 64)) return (int)hipErrorInvalidValue;
+  if (a->in_fin.stats != nullptr &&
+      (a->in_scale == nullptr || a->in_fin.C != a->C || a->in_fin.G < 1 || a->in_fin.G > DRN_BN_FIN_GMAX))
+    return (int)hipErrorInvalidValue;
   if (drn_conv_glds_ok(a) && zero != nullptr && a->cfg != 100)
     return drn::launch_glds_cfg(a->cfg >= 0 ? a->cfg : drn::glds_default_cfg(a), a, zero, s);
+  if (a->in_fin.stats != nullptr) {
+    if (a->in_fin.publish) {  // non-publishing consumers read the already published parameters
+      const int rc = drn_bn_fin_fwd_launch(&a->in_fin, s);
+      if (rc) return rc;
+    }
+    DrnConvFwdArgs b = *a;
+    b.in_fin.stats = nullptr;
+    return drn_conv_fwd(&b, s);
+  }
   return drn_conv_fwd(a, s);
 }
 

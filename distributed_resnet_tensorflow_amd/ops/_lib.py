@@ -37,6 +37,15 @@ class DrnFastDiv(ctypes.Structure):
         return cls(d, m & 0xFFFFFFFF, s, 0)
 
 
+class DrnBnFin(ctypes.Structure):
+    """Mirror of csrc/include/drn_conv.h `struct DrnBnFin` (consumer-side BatchNorm finalize)."""
+    _fields_ = [
+        ("stats", c_p), ("gamma", c_p), ("beta", c_p), ("run_mean", c_p), ("run_var", c_p), ("scale", c_p),
+        ("shift", c_p), ("mean", c_p), ("invstd", c_p), ("dgamma", c_p), ("dbeta", c_p),
+        ("G", c_int), ("C", c_int), ("count", c_f), ("eps", c_f), ("momentum", c_f), ("publish", c_int),
+    ]
+
+
 class DrnConvFwdArgs(ctypes.Structure):
     _fields_ = [
         ("x", c_p), ("w", c_p), ("y", c_p), ("in_scale", c_p), ("in_shift", c_p), ("residual", c_p), ("stats", c_p),
@@ -51,7 +60,7 @@ class DrnConvFwdArgs(ctypes.Structure):
         ("fin_gamma", c_p), ("fin_beta", c_p), ("fin_run_mean", c_p), ("fin_run_var", c_p),
         ("fin_scale", c_p), ("fin_shift", c_p), ("fin_mean", c_p), ("fin_invstd", c_p),
         ("fin_dgamma", c_p), ("fin_dbeta", c_p), ("fin_coef", c_p),
-        ("fd_pq", DrnFastDiv), ("fd_q", DrnFastDiv),
+        ("fd_pq", DrnFastDiv), ("fd_q", DrnFastDiv), ("in_fin", DrnBnFin),
     ]
 
 
@@ -105,6 +114,11 @@ _SIGS = {
     "drn_p2p_reduce2": ([c_p, c_int, c_p], c_int),
     "drn_p2p_wait": ([c_p, c_p, c_p], c_int),
     "drn_p2p_args_size": ([], c_int),
+    "drn_bn_fin_size": ([], c_int),
+    "drn_conv_args_size": ([], c_int),
+    "drn_bn_fin_fwd_launch": ([c_p, c_p], c_int),
+    "drn_bn_apply_fin": ([c_p, c_p, c_p, c_i64, c_int, c_int, c_p], c_int),
+    "drn_bn_bwd_apply_fin": ([c_p, c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_p], c_int),
     "drn_synthetic_images": ([c_p, c_i64, ctypes.c_uint32, c_p], c_int),
 }
 
@@ -140,6 +154,9 @@ def lib():
             fn = getattr(h, name)
             fn.argtypes = args
             fn.restype = res
+        for name, st in (("drn_bn_fin_size", DrnBnFin), ("drn_conv_args_size", DrnConvFwdArgs)):
+            if getattr(h, name)() != ctypes.sizeof(st):
+                raise KernelLibraryError(f"{st.__name__} layout mismatch between Python and {LIB_PATH.name}")
         _LIB = h
         return _LIB
 

@@ -108,6 +108,49 @@ class BnFin:
     eps: float = 1e-5
 
 
+@dataclass
+class BnCfin:
+    """Consumer-side BatchNorm finalize (csrc/include/drn_conv.h DrnBnFin): the kernel that
+    CONSUMES a BatchNorm derives its parameters from the statistics replicas `stats` [G][2][C]
+    in its own prologue instead of a separate finalize launch; with `publish` its first workgroup
+    also writes them out (forward: scale/shift/mean/invstd + moving averages; backward: dgamma,
+    dbeta) for the kernels that run later."""
+    stats: torch.Tensor
+    count: float
+    gamma: torch.Tensor
+    beta: Optional[torch.Tensor] = None
+    run_mean: Optional[torch.Tensor] = None
+    run_var: Optional[torch.Tensor] = None
+    scale: Optional[torch.Tensor] = None
+    shift: Optional[torch.Tensor] = None
+    mean: Optional[torch.Tensor] = None
+    invstd: Optional[torch.Tensor] = None
+    dgamma: Optional[torch.Tensor] = None
+    dbeta: Optional[torch.Tensor] = None
+    publish: bool = False
+    momentum: float = 0.997
+    eps: float = 1e-5
+
+    @property
+    def C(self) -> int:
+        return self.gamma.numel()
+
+    @property
+    def G(self) -> int:
+        return self.stats.numel() // (2 * self.C)
+
+    def struct(self):
+        f = _lib.DrnBnFin()
+        f.stats, f.gamma, f.beta = self.stats.data_ptr(), self.gamma.data_ptr(), _ptr(self.beta)
+        f.run_mean, f.run_var = _ptr(self.run_mean), _ptr(self.run_var)
+        f.scale, f.shift, f.mean, f.invstd = _ptr(self.scale), _ptr(self.shift), _ptr(self.mean), _ptr(self.invstd)
+        f.dgamma, f.dbeta = _ptr(self.dgamma), _ptr(self.dbeta)
+        f.G, f.C = self.G, self.C
+        f.count, f.eps, f.momentum = float(self.count), float(self.eps), float(self.momentum)
+        f.publish = 1 if self.publish else 0
+        return f
+
+
 @dataclass(frozen=True)
 class OutMap:
     """Strided output mapping of a phase of a stride-2 data gradient: the GEMM's P x Q grid lands
@@ -146,6 +189,29 @@ class _Common:
         self.bn_bwd_apply(dy, dpool, pool_hw, x, scale, shift, mean, invstd, coef, add, dx, relu=relu)
 
 
+    def fill_(self, t, v: float):
+        t.fill_(v)
+
+    # Consumer-side finalize (BnCfin) composed from the separate ops; HIP overrides with kernels
+    # that finalize in their prologue.
+    def _publish_fwd(self, f: BnCfin):
+        self.bn_finalize(f.stats, f.G, f.count, f.gamma, f.beta, f.run_mean, f.run_var, f.scale, f.shift, f.mean,
+                         f.invstd, f.momentum, f.eps, update_running=f.run_mean is not None)
+
+    def bn_apply_fin(self, x, y, fin: BnCfin, relu=True):
+        if fin.publish:
+            self._publish_fwd(fin)
+        self.bn_apply(x, y, fin.scale, fin.shift, relu=relu)
+
+    def bn_bwd_apply_fin(self, dy, dpool, pool_hw, x, scale, shift, fin: BnCfin, add, dx, relu=True):
+        C = fin.C
+        coef = torch.empty(3 * C, dtype=fin.gamma.dtype, device=x.device)
+        dg = fin.dgamma if fin.publish else torch.empty_like(fin.gamma)
+        db = fin.dbeta if fin.publish else torch.empty_like(fin.gamma)
+        self.bn_finalize_bwd(fin.stats, fin.G, fin.count, fin.gamma, fin.invstd, dg, db, coef)
+        self.bn_bwd_apply(dy, dpool, pool_hw, x, scale, shift, fin.mean, fin.invstd, coef, add, dx, relu=relu)
+
+
 class HipBackend(_Common):
     name = "hip"
     act_dtype = torch.bfloat16
@@ -174,7 +240,7 @@ class HipBackend(_Common):
 
     # -- conv ---------------------------------------------------------------------------------
     def conv_args(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None,
-                  bn_bwd=None, bn_fin: Optional[BnFin] = None):
+                  bn_bwd=None, bn_fin: Optional[BnFin] = None, in_fin: Optional[BnCfin] = None):
         N, H, W, C = x.shape
         K, R, S, C2 = w.shape
         N2, P, Q, K2 = y.shape
@@ -219,6 +285,10 @@ class HipBackend(_Common):
                 a.fin_run_mean, a.fin_run_var = _ptr(f.run_mean), _ptr(f.run_var)
                 a.fin_scale, a.fin_shift = f.scale.data_ptr(), f.shift.data_ptr()
                 a.fin_mean, a.fin_invstd = f.mean.data_ptr(), f.invstd.data_ptr()
+        if in_fin is not None:
+            assert in_bn is not None and in_fin.C == C, "the consumer-side finalize feeds the fused BN prologue"
+            _aligned16(in_fin.stats)
+            a.in_fin = in_fin.struct()
         a.cfg = self.forced_cfg if self.forced_cfg is not None else self.conv_cfg.get(self.conv_key(a), -1)
         return a
 
@@ -256,6 +326,7 @@ class HipBackend(_Common):
         if a.stats is not None:
             t.stats = st.data_ptr()
         t.fin_cnt = None  # timing runs must not finalize (moving averages) the live BN
+        t.in_fin.publish = 0
         best, best_t = 100, float("inf")
         s = self.stream()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -279,12 +350,13 @@ class HipBackend(_Common):
         return best
 
     def conv_fwd(self, x, w, y, g, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None, bn_bwd=None,
-                 bn_fin: Optional[BnFin] = None, out_fill: bool = False):
+                 bn_fin: Optional[BnFin] = None, out_fill: bool = False, in_fin: Optional[BnCfin] = None):
         """y = conv(x) (+ residual); optional BN statistics of y, or (bn_bwd = (x_bn, scale, shift,
         mean, invstd)) the fused BN-backward reduction with ReLU-masked output; bn_fin finalizes
         that BN in the same launch. out_fill (strided out_map, single-phase output): the epilogue
-        also writes zeros at every other phase position, so y needs no separate clearing."""
-        a = self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd, bn_fin)
+        also writes zeros at every other phase position, so y needs no separate clearing.
+        in_fin: the input BN (in_bn) is finalized by this conv's prologue (BnCfin)."""
+        a = self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd, bn_fin, in_fin)
         if out_fill:
             assert out_map is not None and bn_bwd is None and residual is None, "out_fill: plain strided output only"
             a.out_fill = 1
@@ -441,6 +513,21 @@ class HipBackend(_Common):
                                                  dbeta.data_ptr(), _ptr(add), dx.data_ptr(), x.numel() // C, C,
                                                  1 if relu else 0, self.stream()), "drn_bn_bwd_apply_stats")
 
+    def bn_apply_fin(self, x, y, fin: BnCfin, relu=True):
+        C = x.shape[-1]
+        f = fin.struct()
+        _lib.check(self.L.drn_bn_apply_fin(x.data_ptr(), y.data_ptr(), ctypes.byref(f), x.numel() // C, C,
+                                           1 if relu else 0, self.stream()), "drn_bn_apply_fin")
+
+    def bn_bwd_apply_fin(self, dy, dpool, pool_hw, x, scale, shift, fin: BnCfin, add, dx, relu=True):
+        C = x.shape[-1]
+        _aligned16(scale, shift)
+        f = fin.struct()
+        _lib.check(self.L.drn_bn_bwd_apply_fin(_ptr(dy), _ptr(dpool), pool_hw, x.data_ptr(), scale.data_ptr(),
+                                               shift.data_ptr(), ctypes.byref(f), _ptr(add), dx.data_ptr(),
+                                               x.numel() // C, C, 1 if relu else 0, self.stream()),
+                   "drn_bn_bwd_apply_fin")
+
     def bn_bwd_reduce(self, dy, dpool, pool_hw, x, scale, shift, mean, invstd, part, relu=True):
         C = x.shape[-1]
         M = x.numel() // C
@@ -529,7 +616,17 @@ class HipBackend(_Common):
                                            self.stream()), "drn_weight_tflip")
 
     def zero_(self, t):
-        t.zero_()
+        """In-tree fill kernel (no PyTorch kernel in the step): fp32 buffers, or any contiguous
+        buffer whose byte size is a multiple of 4 (zero bits are zero in every dtype)."""
+        nb = t.numel() * t.element_size()
+        if t.is_contiguous() and nb % 4 == 0 and t.data_ptr() % 4 == 0:
+            _lib.check(self.L.drn_fill_f32(t.data_ptr(), nb // 4, 0.0, self.stream()), "drn_fill_f32")
+        else:
+            t.zero_()
+
+    def fill_(self, t, v: float):
+        assert t.dtype == torch.float32 and t.is_contiguous()
+        _lib.check(self.L.drn_fill_f32(t.data_ptr(), t.numel(), float(v), self.stream()), "drn_fill_f32")
 
     # -- input ----------------------------------------------------------------------------------
     def cifar_augment(self, raw_u8, params_i32, out, pad):
@@ -594,7 +691,9 @@ class RefBackend(_Common):
         return None
 
     def conv_fwd(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None,
-                 bn_bwd=None, bn_fin: Optional[BnFin] = None, out_fill: bool = False):
+                 bn_bwd=None, bn_fin: Optional[BnFin] = None, out_fill: bool = False, in_fin: Optional[BnCfin] = None):
+        if in_fin is not None and in_fin.publish:
+            self._publish_fwd(in_fin)
         self._conv_fwd(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd, out_fill)
         if bn_fin is not None:
             f, G = bn_fin, stats.numel() // (2 * w.shape[0])

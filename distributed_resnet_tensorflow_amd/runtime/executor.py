@@ -30,7 +30,7 @@ from typing import Callable, List, Optional
 import torch
 
 from ..models.spec import Block, BN, Conv, NetSpec
-from ..ops.backend import BnFin, ConvGeom, OutMap, dgrad_geom, tflip_desc, tflip_table
+from ..ops.backend import BnCfin, BnFin, ConvGeom, OutMap, dgrad_geom, tflip_desc, tflip_table
 from .params import ParamStore
 
 BN_DECAY = 0.997     # reference resnet_model_official.py:37
@@ -61,6 +61,7 @@ class BNState:
     fin_b: Optional[torch.Tensor] = None   # ... and of the fused backward finalize
     fin_done: bool = False                 # this step's forward finalize ran inside the producer conv
     bfin_done: bool = False                # this step's backward finalize ran inside the dgrad
+    cfin_pub: bool = False                 # consumer-side finalize: the next consumer publishes
 
     @property
     def ss(self):
@@ -129,6 +130,12 @@ class Executor:
         # before it retires -- measured 12.85 ms vs 11.78 ms per ResNet-50 step, so off
         self.fuse_fin = os.environ.get("DRN_FUSE_BN_FIN", "0") == "1" and not self.deterministic
         self.fuse_finalize_fwd = os.environ.get("DRN_FUSE_BN_FINALIZE_FWD", "0") == "1"
+        # Consumer-side BN finalize (DRN_CFIN, default on for HIP): no finalize launches at all --
+        # the kernels CONSUMING a BatchNorm (the fused-prologue 1x1 convs, the materialising
+        # apply, the backward apply) derive its parameters from the statistics replicas in their
+        # own prologue and the first of them publishes them (ops/backend.py BnCfin). Removes ~98
+        # dependent ~6 us launches per ResNet-50 step from the critical path.
+        self.cfin = not self.deterministic and not self.fuse_fin and os.environ.get("DRN_CFIN", "1") == "1"
         # single-phase strided data gradients zero the other phases in their own epilogue
         self.out_fill = os.environ.get("DRN_OUT_FILL", "1") == "1"
         self.device = torch.device(device)
@@ -238,10 +245,17 @@ class Executor:
         receives exactly one atomic add and the finalize sums the slots in a fixed order."""
         return max(((M + 63) // 64) * ((C + 63) // 64), 1024)
 
+    def _reps(self, C: int) -> int:
+        """Atomic-spreading replicas of a C-channel statistics accumulator: the backend's count up
+        to 256 channels, fewer for wide BNs (whose producers have few pixel tiles, and whose
+        consumers re-read all 2*R*C sums in every workgroup's finalize prologue)."""
+        r = max(1, min(self.stats_rep, self.stats_rep * 256 // C))
+        return min(r, 8) if self.cfin else r   # the finalizing consumers sum at most 8 replicas
+
     def _stats_for(self, M: int, C: int) -> tuple[torch.Tensor, int]:
         """A [R][2][C] statistics accumulator (R = the backend's atomic-spreading replicas)
         carved from the per-step-cleared arena."""
-        R = self._det_replicas(M, C) if self.deterministic else self.stats_rep
+        R = self._det_replicas(M, C) if self.deterministic else self._reps(C)
         n = (2 * C * R + 15) // 16 * 16
         if self._arena_off + n > self._arena_cap:
             raise RuntimeError("statistics arena exhausted")
@@ -280,7 +294,7 @@ class Executor:
         if self.deterministic:
             arena = 64 + sum(2 * ((2 * c * self._det_replicas(m, c) + 15) // 16 * 16) for m, c in self._bn_shapes())
         else:
-            arena = sum(2 * ((2 * c * self.stats_rep + 15) // 16 * 16) for c in all_c) + 64
+            arena = sum(2 * ((2 * c * self._reps(c) + 15) // 16 * 16) for c in all_c) + 64
         # + the arrival counters of the fused finalizes (64 per BN and direction), cleared with
         # the statistics by the same per-step fill
         n_bn = len(all_c) + 1
@@ -431,7 +445,27 @@ class Executor:
     # ------------------------------------------------------------------------------------------
     # forward
     # ------------------------------------------------------------------------------------------
+    def _fin_fwd_spec(self, b: BNState, publish: bool) -> BnCfin:
+        return BnCfin(b.stats, float(b.rows), b.gamma, beta=b.beta, run_mean=b.run_mean, run_var=b.run_var,
+                      scale=b.scale, shift=b.shift, mean=b.mean, invstd=b.invstd, publish=publish,
+                      momentum=BN_DECAY, eps=BN_EPSILON)
+
+    def _take_fin(self, b: BNState) -> Optional[BnCfin]:
+        """The consumer-side finalize for the next kernel consuming relu(bn(b.src)) through its
+        fused prologue: only the first consumer of the step finalizes (and publishes); later ones
+        read the published scale/shift."""
+        if not b.cfin_pub:
+            return None
+        b.cfin_pub = False
+        return self._fin_fwd_spec(b, publish=True)
+
     def _bn_fwd(self, b: BNState, train: bool):
+        if train and self.cfin and b is not self.final_bn:
+            if b.act is not None:  # materialised for a 3x3 consumer: the apply finalizes
+                self.be.bn_apply_fin(b.src, b.act, self._fin_fwd_spec(b, publish=True), relu=True)
+            else:
+                b.cfin_pub = True
+            return
         if train and b.fin_done:  # finalized by the producing conv
             b.fin_done = False
             if b.act is not None:
@@ -450,10 +484,11 @@ class Executor:
         if b.act is not None:
             self.be.bn_apply(b.src, b.act, b.scale, b.shift, relu=True)
 
-    @staticmethod
-    def _cin(b: BNState):
-        """(tensor, in_bn) a conv consuming relu(bn(b.src)) reads."""
-        return (b.act, None) if b.act is not None else (b.src, b.ss)
+    def _cin(self, b: BNState):
+        """(tensor, in_bn, in_fin) a conv consuming relu(bn(b.src)) reads."""
+        if b.act is not None:
+            return b.act, None, None
+        return b.src, b.ss, self._take_fin(b)
 
     def forward(self, train: bool = True):
         """Runs the network on self.images/self.labels; fills loss_vec/correct (and dlogits)."""
@@ -504,17 +539,17 @@ class Executor:
         bn = bp.bn
         self._bn_fwd(bn[0], train)
         if bp.proj is not None:
-            xin, pro = self._cin(bn[0])
-            be.conv_fwd(xin, bp.proj.w, bp.sc, bp.proj.geom, in_bn=pro)
+            xin, pro, fin = self._cin(bn[0])
+            be.conv_fwd(xin, bp.proj.w, bp.sc, bp.proj.geom, in_bn=pro, in_fin=fin)
         for i, op in enumerate(bp.convs):
             last = i == len(bp.convs) - 1
-            xin, pro = self._cin(bn[i])
+            xin, pro, fin = self._cin(bn[i])
             if last:
                 res = bp.sc if bp.proj is not None else bp.x
-                be.conv_fwd(xin, op.w, bp.out, op.geom, in_bn=pro, residual=res,
+                be.conv_fwd(xin, op.w, bp.out, op.geom, in_bn=pro, residual=res, in_fin=fin,
                             stats=bp.out_stats if train else None, bn_fin=self._fin_fwd(bp.out_stats, train))
             else:
-                be.conv_fwd(xin, op.w, bp.hs[i], op.geom, in_bn=pro,
+                be.conv_fwd(xin, op.w, bp.hs[i], op.geom, in_bn=pro, in_fin=fin,
                             stats=bn[i + 1].stats if train else None, bn_fin=self._fin_fwd(bn[i + 1].stats, train))
                 self._bn_fwd(bn[i + 1], train)
 
@@ -534,6 +569,11 @@ class Executor:
         G = b.bG
         if not reduced:
             G = be.bn_bwd_reduce(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, part)
+        if self.cfin:  # finalize in the apply's prologue; it publishes dgamma / dbeta
+            fin = BnCfin(part, float(M), b.gamma, mean=b.mean, invstd=b.invstd, dgamma=b.dgamma, dbeta=b.dbeta,
+                         publish=True)
+            be.bn_bwd_apply_fin(dy, dpool, pool_hw, x, b.scale, b.shift, fin, add, dx, relu=not reduced)
+            return
         coef = self.bn_coef[:3 * b.bn.c]
         if b.bfin_done:  # finalized by the producing data-gradient conv
             b.bfin_done = False
@@ -672,7 +712,7 @@ class Executor:
             op, xin, b = bp.convs[i], ins[i], bp.bn[i]
             tgt_k = self._take(bufs, (cur, dy_k))
             tgt = bufs[tgt_k]
-            a_in, pro = self._cin(b)
+            a_in, pro = (b.act, None) if b.act is not None else (b.src, b.ss)
             self._wgrad(a_in, dy, op.dw, op.geom, in_bn=pro, dy_buf=dy_buf)
             self._claim(tgt)
             da = self._view(tgt, xin)        # d relu(bn(xin))
@@ -705,7 +745,7 @@ class Executor:
     # optimizer
     # ------------------------------------------------------------------------------------------
     def set_lr(self, lr: float):
-        self.lr_t.fill_(float(lr))
+        self.be.fill_(self.lr_t, float(lr))
 
     def apply_gradients(self, grad_scale: float = 1.0, grad: Optional[torch.Tensor] = None):
         P = self.P

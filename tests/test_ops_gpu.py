@@ -556,3 +556,77 @@ def test_conv_fused_bn_finalize(hip, ref, cfg, bwd):
     keys = ("dgamma", "dbeta", "coef") if bwd else ("scale", "shift", "mean", "invstd", "run_mean", "run_var")
     for k in keys:
         assert rel(got[k], exp[k]) < 2e-2, (k, rel(got[k], exp[k]))
+
+
+@pytest.mark.parametrize("C,G", [(64, 8), (256, 8), (1024, 2), (2048, 1)])
+@pytest.mark.parametrize("relu_bwd", [True, False])
+def test_bn_consumer_finalize(hip, ref, C, G, relu_bwd):
+    """Consumer-side BN finalize (BnCfin): the materialising apply and the backward apply derive
+    the BN parameters from G statistics replicas in their prologue and publish them (moving
+    averages, dgamma/dbeta); compared with the separate finalize + apply of the fp32 reference."""
+    from distributed_resnet_tensorflow_amd.ops.backend import BnCfin
+    torch.manual_seed(11)
+    N, H = 4, 6
+    x = bf(torch.randn(N, H, H, C) * 1.5 + 0.3)
+    dy0, add0 = bf(torch.randn(N, H, H, C)), bf(torch.randn(N, H, H, C))
+    gamma, beta = torch.rand(C) + 0.5, torch.randn(C) * 0.2
+    M = N * H * H
+    xf = x.float().reshape(M, C)
+    # the same sums split over G replicas (as the atomic-spreading producers leave them)
+    tot = torch.stack([xf.sum(0), (xf * xf).sum(0)])
+    w = torch.rand(G, 1, 1)
+    w = w / w.sum()
+    parts = (tot.unsqueeze(0) * w).contiguous()
+    outs = {}
+    for be, dev in ((ref, "cpu"), (hip, "cuda")):
+        xx = x.to(dev) if dev == "cuda" else x.float()
+        st = parts.to(dev) if dev == "cuda" else parts.sum(0, keepdim=True).clone()
+        rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+        sc, sh, mu, isd = (torch.zeros(C, device=dev) for _ in range(4))
+        fin = BnCfin(st, float(M), gamma.to(dev), beta=beta.to(dev), run_mean=rm, run_var=rv, scale=sc, shift=sh,
+                     mean=mu, invstd=isd, publish=True)
+        y = torch.zeros_like(xx)
+        be.bn_apply_fin(xx, y, fin, relu=True)
+        dy = dy0.to(dev) if dev == "cuda" else dy0.float()
+        add = add0.to(dev) if dev == "cuda" else add0.float()
+        # backward sums (sum g, sum g*xhat) of the masked gradient, again split over replicas
+        g = dy.float().reshape(M, C) * ((xx.float().reshape(M, C) * sc + sh) > 0).float() if relu_bwd \
+            else dy.float().reshape(M, C)
+        xh = (xx.float().reshape(M, C) - mu) * isd
+        btot = torch.stack([g.sum(0), (g * xh).sum(0)])
+        bst = (btot.unsqueeze(0) * w.to(btot.device)).contiguous() if dev == "cuda" else btot.unsqueeze(0).clone()
+        dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+        bfin = BnCfin(bst, float(M), gamma.to(dev), mean=mu, invstd=isd, dgamma=dg, dbeta=db, publish=True)
+        dx = torch.zeros_like(xx)
+        be.bn_bwd_apply_fin(dy, None, 0, xx, sc, sh, bfin, add, dx, relu=relu_bwd)
+        outs[be.name] = [t.float().cpu() for t in (sc, sh, mu, isd, rm, rv, y, dg, db, dx)]
+    for name, a, b in zip("sc sh mu isd rm rv y dg db dx".split(), outs["hip"], outs["ref"]):
+        assert rel(a, b) < 1e-2, name
+
+
+@pytest.mark.parametrize("publish", [True, False])
+def test_conv_prologue_finalize(hip, ref, publish):
+    """A fused-prologue 1x1 conv finalizing its input BN from the statistics replicas equals the
+    conv reading separately finalized scale/shift; only a publishing launch writes them out."""
+    from distributed_resnet_tensorflow_amd.ops.backend import BnCfin
+    torch.manual_seed(12)
+    N, H, C, K = 2, 14, 128, 256
+    x = bf(torch.randn(N, H, H, C) + 0.2).cuda()
+    wgt = bf(torch.randn(K, 1, 1, C) * 0.05).cuda()
+    gamma, beta = (torch.rand(C) + 0.5).cuda(), (torch.randn(C) * 0.2).cuda()
+    xf = x.float().reshape(-1, C)
+    st = (torch.stack([xf.sum(0), (xf * xf).sum(0)]).unsqueeze(0) / 4).repeat(4, 1, 1).contiguous()
+    sc0, sh0, mu0, is0 = (torch.zeros(C, device="cuda") for _ in range(4))
+    hip.bn_finalize(st, 4, xf.shape[0], gamma, beta, None, None, sc0, sh0, mu0, is0, 0.997, 1e-5, update_running=False)
+    want = torch.empty(N, H, H, K, dtype=torch.bfloat16, device="cuda")
+    hip.conv_fwd(x, wgt, want, ConvGeom(1, 0, 0), in_bn=(sc0, sh0))
+    sc, sh, mu, isd = (torch.full((C,), 7.0, device="cuda") for _ in range(4))
+    fin = BnCfin(st, float(xf.shape[0]), gamma, beta=beta, scale=sc, shift=sh, mean=mu, invstd=isd, publish=publish)
+    got = torch.empty_like(want)
+    hip.conv_fwd(x, wgt, got, ConvGeom(1, 0, 0), in_bn=(sc, sh), in_fin=fin)
+    torch.cuda.synchronize()
+    assert rel(got, want) < 1e-2
+    if publish:
+        assert rel(sc, sc0) < 1e-5 and rel(sh, sh0) < 1e-4 and rel(isd, is0) < 1e-5
+    else:
+        assert bool((sc == 7.0).all())
