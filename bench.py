@@ -46,8 +46,11 @@ def main():
     ap.add_argument("--batch_size", type=int, default=128, help="per-GPU batch")
     ap.add_argument("--graph", type=int, default=-1, help="capture the step in a HIP graph (-1: auto)")
     ap.add_argument("--bucket_mb", type=float, default=25.0)
-    ap.add_argument("--allreduce", default="rccl", choices=["rccl", "p2p", "auto"])
+    ap.add_argument("--allreduce", default="auto", choices=["rccl", "p2p", "auto"],
+                    help="auto: the one-shot P2P kernel when the whole gradient is <= 64 MB (CIFAR), else RCCL")
     ap.add_argument("--shard_optimizer", type=int, default=0, help="ZeRO-1 sharded optimizer (N > 1)")
+    ap.add_argument("--allreduce_wire", default="fp32", choices=["fp32", "bf16"],
+                    help="gradient dtype on the wire (bf16: half the all-reduce bytes)")
     args = ap.parse_args()
 
     import torch
@@ -68,7 +71,14 @@ def main():
     if force_dp and world == 1 and "MASTER_ADDR" not in os.environ:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("DRN_BENCH_PORT", "29533"),
                           RANK="0", WORLD_SIZE="1")
-    if (world > 1 or force_dp or args.graph == 0) and args.graph != 1:
+    from distributed_resnet_tensorflow_amd.models.spec import build_spec
+    spec = build_spec(args.dataset, args.resnet_size, width=args.width)
+    # the P2P all-reduce (chosen by --allreduce p2p, or auto for <= 64 MB of gradients) runs the
+    # data-parallel step as one HIP graph; RCCL data parallelism runs it eagerly
+    p2p = (world > 1 or force_dp) and (args.allreduce == "p2p" or
+                                       (args.allreduce == "auto" and spec.num_params() * 4 <= 64 << 20))
+    eager_dp = (world > 1 or force_dp) and not p2p
+    if (eager_dp or args.graph == 0) and args.graph != 1:
         # eager data-parallel step: its main (critical-path) stream at HIGH priority -- see
         # parallel.engine.use_priority_main_stream
         from distributed_resnet_tensorflow_amd.parallel.engine import use_priority_main_stream
@@ -79,17 +89,15 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    from distributed_resnet_tensorflow_amd.models.spec import build_spec
     from distributed_resnet_tensorflow_amd.ops.backend import HipBackend
     from distributed_resnet_tensorflow_amd.runtime.executor import Executor
     from distributed_resnet_tensorflow_amd.runtime.graph import SegmentedStepGraph, StepGraph
     from distributed_resnet_tensorflow_amd.parallel.engine import DataParallelEngine
 
-    spec = build_spec(args.dataset, args.resnet_size, width=args.width)
     be = HipBackend("cuda")
     wd = 2e-4 if args.dataset == "cifar10" else 1e-4
     ex = Executor(spec, args.batch_size, be, "cuda", seed=1234, weight_decay=wd)
-    eng = DataParallelEngine(ex, bucket_mb=args.bucket_mb, allreduce=args.allreduce,
+    eng = DataParallelEngine(ex, bucket_mb=args.bucket_mb, allreduce=args.allreduce, wire=args.allreduce_wire,
                              shard_optimizer=bool(args.shard_optimizer)) if (world > 1 or force_dp) else None
     if eng is not None:
         eng.broadcast_parameters()
@@ -116,7 +124,9 @@ def main():
     # with the single-rank RCCL engine, eager 11.90 ms vs per-segment graphs (--graph 1,
     # runtime/graph.py SegmentedStepGraph, bucket all-reduces issued between graphs) 12.22 ms:
     # the ~20 graph launches cost more than the host-side kernel launches they replace
-    use_graph = args.graph if args.graph >= 0 else int(eng is None)
+    # (the P2P all-reduce is a set of kernels with device-side flags: a data-parallel step on it is
+    # captured whole, comm included -- SURVEY §5.8)
+    use_graph = args.graph if args.graph >= 0 else int(eng is None or eng.p2p is not None)
     run = step
     if eng is not None and eng.zero1:
         use_graph = 0

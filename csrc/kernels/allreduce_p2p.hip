@@ -62,11 +62,10 @@ __device__ __forceinline__ bool wait_all(const P2PArgs& a, int kind, unsigned e)
   return false;
 }
 
-// kind = READY or DONE: publish this rank's epoch for `slot` to every rank (incl. itself).
-__global__ void p2p_signal_kernel(P2PArgs a, int kind) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const unsigned e = *a.epoch;
-  // make every earlier write of this device (the gradient kernels) visible system-wide
+// publish this rank's epoch e for (slot, kind) to every rank (incl. itself); one thread. The
+// system-scope release makes every earlier write of this device (the gradient kernels, the bf16
+// wire cast) visible to the peers reading it over xGMI.
+__device__ __forceinline__ void publish(const P2PArgs& a, int kind, unsigned e) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   for (int r = 0; r < a.world; ++r) {
     unsigned* f = a.flags_peer[r] + (size_t)(a.slot * P2P_KINDS + kind) * P2P_MAX_RANKS + a.rank;
@@ -74,20 +73,49 @@ __global__ void p2p_signal_kernel(P2PArgs a, int kind) {
   }
 }
 
+// kind = READY or DONE: publish this rank's epoch for `slot` (kept for the two-shot RS_DONE).
+__global__ void p2p_signal_kernel(P2PArgs a, int kind) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  publish(a, kind, *a.epoch);
+}
+
+// wire element -> fp32 accumulate
+template <typename W>
+__device__ __forceinline__ float4 load4(const W* p, int64_t i);
+template <>
+__device__ __forceinline__ float4 load4<float>(const float* p, int64_t i) {
+  return reinterpret_cast<const float4*>(p)[i];
+}
+template <>
+__device__ __forceinline__ float4 load4<bf16_t>(const bf16_t* p, int64_t i) {
+  const uint2 u = reinterpret_cast<const uint2*>(p)[i];
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+
+// Signal + wait + reduce of one bucket in ONE launch: workgroup 0 publishes this rank's READY
+// (the bucket is complete: the launch is stream-ordered after its producers), every workgroup
+// polls its local flags for all ranks, acquires, and reduces out[i] = sum_r in_r[i] (fp32
+// accumulate in rank order: identical on every rank, bitwise reproducible). W = wire type of the
+// inputs (fp32, or bf16 shadows written by drn_p2p_cast).
+template <typename W>
 __global__ __launch_bounds__(256) void p2p_reduce_kernel(P2PArgs a) {
   __shared__ int ok;
+  const unsigned e = *a.epoch;
   if (threadIdx.x == 0) {
-    ok = wait_all(a, P2P_READY, *a.epoch) ? 1 : 0;
+    if (blockIdx.x == 0) publish(a, P2P_READY, e);
+    ok = wait_all(a, P2P_READY, e) ? 1 : 0;
     if (!ok) atomicExch(a.err, 1);
   }
   __syncthreads();
   if (!ok) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // peers' gradient bytes, not stale cached lines
   const int64_t n4 = a.n / 4;
+  const W* const* in = reinterpret_cast<const W* const*>(a.in);
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    float4 s = reinterpret_cast<const float4*>(a.in[0])[i];
+    float4 s = load4<W>(in[0], i);
     for (int r = 1; r < a.world; ++r) {
-      const float4 v = reinterpret_cast<const float4*>(a.in[r])[i];
+      const float4 v = load4<W>(in[r], i);
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
     reinterpret_cast<float4*>(a.out)[i] = s;
@@ -102,11 +130,14 @@ __device__ __forceinline__ void shard_of(const P2PArgs& a, int r, int64_t& lo, i
   hi = lo + sh < n4 ? lo + sh : n4;
 }
 
-// reduce-scatter: my shard = sum over ranks of their inputs' shard
+// reduce-scatter (+ READY publish): my shard = sum over ranks of their inputs' shard
+template <typename W>
 __global__ __launch_bounds__(256) void p2p_rs_kernel(P2PArgs a) {
   __shared__ int ok;
+  const unsigned e = *a.epoch;
   if (threadIdx.x == 0) {
-    ok = wait_all(a, P2P_READY, *a.epoch) ? 1 : 0;
+    if (blockIdx.x == 0) publish(a, P2P_READY, e);
+    ok = wait_all(a, P2P_READY, e) ? 1 : 0;
     if (!ok) atomicExch(a.err, 1);
   }
   __syncthreads();
@@ -114,10 +145,11 @@ __global__ __launch_bounds__(256) void p2p_rs_kernel(P2PArgs a) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   int64_t lo, hi;
   shard_of(a, a.rank, lo, hi);
+  const W* const* in = reinterpret_cast<const W* const*>(a.in);
   for (int64_t i = lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < hi; i += (int64_t)gridDim.x * blockDim.x) {
-    float4 s = reinterpret_cast<const float4*>(a.in[0])[i];
+    float4 s = load4<W>(in[0], i);
     for (int r = 1; r < a.world; ++r) {
-      const float4 v = reinterpret_cast<const float4*>(a.in[r])[i];
+      const float4 v = load4<W>(in[r], i);
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
     reinterpret_cast<float4*>(a.out)[i] = s;
@@ -145,14 +177,28 @@ __global__ __launch_bounds__(256) void p2p_ag_kernel(P2PArgs a) {
   }
 }
 
-// Wait until every rank published DONE for `slot` at the previous epoch, then advance the
-// device epoch (one thread; launched once per step before the gradient buffer is rewritten).
-__global__ void p2p_wait_kernel(P2PArgs a, unsigned* epoch_rw) {
+// Step boundary, one thread, ONE launch per step (before the step writes the gradient buffer):
+// publish DONE for the finished epoch e (this rank's reductions of step e were stream-ordered
+// before this launch, so it no longer reads any peer's buffers), wait until every rank published
+// DONE >= e (no rank overwrites an input or output buffer a peer may still be reading), then
+// advance the device epoch.
+__global__ void p2p_step_kernel(P2PArgs a, unsigned* epoch_rw) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const unsigned e = *epoch_rw;
-  if (e > 0 && !wait_all(a, P2P_DONE, e)) atomicExch(a.err, 2);
+  if (e > 0) {
+    publish(a, P2P_DONE, e);
+    if (!wait_all(a, P2P_DONE, e)) atomicExch(a.err, 2);
+  }
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");
   *epoch_rw = e + 1;
+}
+
+// fp32 bucket -> bf16 wire shadow (round to nearest even), 4 elements per thread
+__global__ __launch_bounds__(256) void p2p_cast_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t n4) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    reinterpret_cast<uint2*>(y)[i] = make_uint2(pack2bf(v.x, v.y), pack2bf(v.z, v.w));
+  }
 }
 
 }  // namespace drn
@@ -171,26 +217,44 @@ DRN_API int drn_p2p_signal(const drn::P2PArgs* a, int kind, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-DRN_API int drn_p2p_reduce(const drn::P2PArgs* a, int blocks, hipStream_t s) {
+// one-shot all-reduce of one bucket (publish + wait + reduce in one launch); wire_bf16: the
+// peers' inputs are bf16 shadows (drn_p2p_cast), accumulated in fp32
+DRN_API int drn_p2p_reduce(const drn::P2PArgs* a, int blocks, int wire_bf16, hipStream_t s) {
   if (!p2p_check(a)) return (int)hipErrorInvalidValue;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(drn::p2p_reduce_kernel, dim3(blocks), dim3(256), 0, s, *a);
+  if (wire_bf16)
+    hipLaunchKernelGGL(drn::p2p_reduce_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, *a);
+  else
+    hipLaunchKernelGGL(drn::p2p_reduce_kernel<float>, dim3(blocks), dim3(256), 0, s, *a);
   return (int)hipGetLastError();
 }
 
-// two-shot all-reduce of one bucket: reduce-scatter, publish RS_DONE, all-gather
-DRN_API int drn_p2p_reduce2(const drn::P2PArgs* a, int blocks, hipStream_t s) {
+// two-shot all-reduce of one bucket: reduce-scatter (with the READY publish), publish RS_DONE,
+// all-gather of the peers' fp32 shards
+DRN_API int drn_p2p_reduce2(const drn::P2PArgs* a, int blocks, int wire_bf16, hipStream_t s) {
   if (!p2p_check(a)) return (int)hipErrorInvalidValue;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(drn::p2p_rs_kernel, dim3(blocks), dim3(256), 0, s, *a);
+  if (wire_bf16)
+    hipLaunchKernelGGL(drn::p2p_rs_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, *a);
+  else
+    hipLaunchKernelGGL(drn::p2p_rs_kernel<float>, dim3(blocks), dim3(256), 0, s, *a);
   hipLaunchKernelGGL(drn::p2p_signal_kernel, dim3(1), dim3(64), 0, s, *a, (int)drn::P2P_RS_DONE);
   hipLaunchKernelGGL(drn::p2p_ag_kernel, dim3(blocks), dim3(256), 0, s, *a);
   return (int)hipGetLastError();
 }
 
-DRN_API int drn_p2p_wait(const drn::P2PArgs* a, unsigned* epoch_rw, hipStream_t s) {
+DRN_API int drn_p2p_step(const drn::P2PArgs* a, unsigned* epoch_rw, hipStream_t s) {
   if (!p2p_check(a)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(drn::p2p_wait_kernel, dim3(1), dim3(64), 0, s, *a, epoch_rw);
+  hipLaunchKernelGGL(drn::p2p_step_kernel, dim3(1), dim3(64), 0, s, *a, epoch_rw);
+  return (int)hipGetLastError();
+}
+
+DRN_API int drn_p2p_cast(const float* x, void* y, int64_t n, hipStream_t s) {
+  if (n % 4) return (int)hipErrorInvalidValue;
+  int64_t b = (n / 4 + 255) / 256;
+  if (b > 1024) b = 1024;
+  if (b < 1) b = 1;
+  hipLaunchKernelGGL(drn::p2p_cast_kernel, dim3((unsigned)b), dim3(256), 0, s, x, (bf16_t*)y, n / 4);
   return (int)hipGetLastError();
 }
 

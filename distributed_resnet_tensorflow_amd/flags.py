@@ -223,6 +223,8 @@ def define_reference_flags(flag_values: FlagValues = FLAGS, **defaults) -> FlagV
     S("profile_steps", "", "a:b -> roctx-mark and torch-profile steps a..b.", fv)
     S("allreduce", "rccl", "Gradient all-reduce: rccl (RCCL ring/tree over xGMI; gloo on CPU), p2p (one-shot "
       "HIP-IPC peer kernel, one node), auto (p2p when the gradient is <= 64 MB).", fv)
+    S("allreduce_wire", "fp32", "Gradient dtype on the wire: fp32, or bf16 (half the all-reduce bytes, fp32 "
+      "accumulation in the P2P kernel; the Horovod fp16-compression analog).", fv)
     Fl("bucket_mb", 25.0, "Gradient all-reduce bucket size cap (MB of fp32).", fv)
     B("optimizer_sharding", False, "ZeRO-1-style sharded optimizer (the parameter-server sharding analog, "
       "SURVEY P3): reduce-scatter the gradient buckets, update 1/N of the weights and momentum per rank, "

@@ -110,9 +110,10 @@ _SIGS = {
     "drn_cifar_augment": ([c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p], c_int),
     "drn_vgg_preprocess": ([c_p, c_p, c_p, c_int, c_int, c_int, c_f, c_f, c_f, c_p], c_int),
     "drn_p2p_signal": ([c_p, c_int, c_p], c_int),
-    "drn_p2p_reduce": ([c_p, c_int, c_p], c_int),
-    "drn_p2p_reduce2": ([c_p, c_int, c_p], c_int),
-    "drn_p2p_wait": ([c_p, c_p, c_p], c_int),
+    "drn_p2p_reduce": ([c_p, c_int, c_int, c_p], c_int),
+    "drn_p2p_reduce2": ([c_p, c_int, c_int, c_p], c_int),
+    "drn_p2p_step": ([c_p, c_p, c_p], c_int),
+    "drn_p2p_cast": ([c_p, c_p, c_i64, c_p], c_int),
     "drn_p2p_args_size": ([], c_int),
     "drn_bn_fin_size": ([], c_int),
     "drn_conv_args_size": ([], c_int),

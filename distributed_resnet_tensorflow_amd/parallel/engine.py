@@ -36,6 +36,7 @@ runs behind step t+1's compute (bounded staleness 1, no PS).
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import List, Optional
 
@@ -66,7 +67,7 @@ def use_priority_main_stream():
 class DataParallelEngine:
     def __init__(self, executor, bucket_mb: float = 25.0, mode: str = "sync", group=None,
                  allreduce: str = "rccl", p2p_max_mb: float = 64.0, first_bucket_mb: float = 2.0,
-                 timeout_s: float = 0.0, shard_optimizer: bool = False):
+                 timeout_s: float = 0.0, shard_optimizer: bool = False, wire: str = ""):
         self.ex = executor
         self.P = executor.P
         self.group = group
@@ -77,6 +78,11 @@ class DataParallelEngine:
         # --allreduce: rccl | p2p (one-shot HIP IPC kernel, parallel/p2p.py) | auto (p2p when the
         # whole gradient is small -- latency-bound CIFAR buckets -- and the job is one GPU node)
         self.p2p = None
+        # gradient dtype on the wire (--allreduce_wire / DRN_ALLREDUCE_WIRE): fp32, or bf16 (half
+        # the collective bytes; fp32 master gradients, like Horovod's fp16 compression)
+        self.wire = (wire or os.environ.get("DRN_ALLREDUCE_WIRE", "fp32")).lower()
+        if self.wire not in ("fp32", "bf16"):
+            raise ValueError(f"all-reduce wire type must be fp32 or bf16, got {self.wire!r}")
         total_mb = self.P.total * 4 / (1 << 20)
         want = allreduce == "p2p" or (allreduce == "auto" and total_mb <= p2p_max_mb)
         if want and self.P.grad.is_cuda and mode == "sync" and self.world <= 8 \
@@ -84,8 +90,15 @@ class DataParallelEngine:
             from .p2p import P2PAllReduce
             if len(self.buckets) + 1 >= 64:
                 self.buckets = self._make_buckets(int(self.P.total // 60) + 1)
-            self.p2p = P2PAllReduce(self.P.grad, group)
+            self.p2p = P2PAllReduce(self.P.grad, group, wire=self.wire)
         self.zero1 = bool(shard_optimizer) and self.world > 1 and mode == "sync"
+        if self.zero1 and self.wire != "fp32":
+            raise ValueError("optimizer sharding reduce-scatters fp32 gradients (--allreduce_wire=fp32)")
+        # RCCL bf16 wire: a bf16 shadow of the flat gradient; each bucket is cast into it, reduced
+        # there, and cast back into the fp32 buffer after its collective completes
+        self.wire_buf = None
+        if self.wire == "bf16" and self.p2p is None and mode == "sync":
+            self.wire_buf = torch.zeros(self.P.total, dtype=torch.bfloat16, device=self.P.grad.device)
         if self.zero1:
             if self.p2p is not None:
                 raise ValueError("optimizer sharding uses reduce-scatter / all-gather collectives, not --allreduce=p2p")
@@ -174,6 +187,12 @@ class DataParallelEngine:
             self.launched[i] = True
             return
         t = (self.P.grad if buf is None else buf)[lo:hi]
+        if self.wire_buf is not None and buf is None:
+            w = self.wire_buf[lo:hi]
+            w.copy_(t)                         # fp32 -> bf16 (round to nearest even), stream-ordered
+            self.works.append(dist.all_reduce(w, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+            self.launched[i] = True
+            return
         if self._sharded(lo, hi):
             # in place: this rank's shard of the bucket receives the sum over ranks
             s0, s1 = self._shard(lo, hi)
@@ -211,6 +230,8 @@ class DataParallelEngine:
             for w in self.works:
                 w.wait()
             self._done_works, self.works = self.works, []
+            if self.wire_buf is not None:      # bf16 sums back into the fp32 gradient buffer
+                self.P.grad.copy_(self.wire_buf)
             self.ex.grad_ready = None
             if self.p2p is not None:
                 self.p2p.end_step()

@@ -10,6 +10,13 @@ included, stays capturable in one HIP graph. Buckets of at least `two_shot_min_k
 1/W shard, then all-gather of the peers' reduced shards from their (also IPC-mapped) output
 buffers -- which moves 2(W-1)/W of the bucket per GPU instead of (W-1)x.
 
+Per step: ONE boundary kernel (publish DONE of the previous step, wait for every peer's DONE,
+advance the device epoch) and ONE kernel per bucket (publish READY + wait + reduce; the two-shot
+form adds the RS_DONE publish and the all-gather). `wire="bf16"` (DRN_P2P_WIRE=bf16) halves the
+bytes every GPU pulls over xGMI: each bucket is first cast to a bf16 shadow buffer (also IPC-
+mapped) on the compute stream and the peers read the shadows, accumulating in fp32 (the same
+trade as Horovod's fp16 gradient compression).
+
 Limits: one node, <= 8 ranks, fp32 buckets whose element count is a multiple of 4.
 """
 from __future__ import annotations
@@ -90,7 +97,7 @@ def _export(t: torch.Tensor):
 class P2PAllReduce:
     """Maps every rank's `grad` (and flag words) and reduces buckets of it into `out`."""
 
-    def __init__(self, grad: torch.Tensor, group=None, two_shot_min_kb: int = -1):
+    def __init__(self, grad: torch.Tensor, group=None, two_shot_min_kb: int = -1, wire: str = ""):
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -100,15 +107,23 @@ class P2PAllReduce:
         if self.L.drn_p2p_args_size() != ctypes.sizeof(P2PArgs):
             raise RuntimeError("P2PArgs layout mismatch between Python and the kernel library")
         self.grad = grad
+        self._arg_cache = {}
         self.comm = torch.cuda.Stream(device=grad.device)
         dev = grad.device
         self.two_shot_min = 1024 * (two_shot_min_kb if two_shot_min_kb >= 0 else
                                     int(os.environ.get("DRN_P2P_TWO_SHOT_MIN_KB", "1024")))
+        self.wire = (wire or os.environ.get("DRN_P2P_WIRE", "fp32")).lower()
+        if self.wire not in ("fp32", "bf16"):
+            raise ValueError(f"P2P wire type must be fp32 or bf16, got {self.wire!r}")
         self.out = torch.zeros_like(grad)
         self.flags = torch.zeros(N_SLOTS * N_KINDS * MAX_RANKS, dtype=torch.int32, device=dev)
         self.epoch = torch.zeros(1, dtype=torch.int32, device=dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
-        mine = (_export(grad), _export(self.flags), _export(self.out))
+        # the tensor the peers read: the fp32 gradient itself, or its bf16 wire shadow
+        self.shadow = torch.zeros(grad.numel(), dtype=torch.bfloat16, device=dev) if self.wire == "bf16" else None
+        src = self.shadow if self.shadow is not None else grad
+        self.esize = src.element_size()
+        mine = (_export(src), _export(self.flags), _export(self.out))
         allh = [None] * self.world
         dist.all_gather_object(allh, pickle.dumps(mine), group=group)
         self._opened = []
@@ -117,7 +132,7 @@ class P2PAllReduce:
         for r, blob in enumerate(allh):
             (gh, goff), (fh, foff), (oh, ooff) = pickle.loads(blob)
             if r == self.rank:
-                self.in_ptr.append(grad.data_ptr())
+                self.in_ptr.append(src.data_ptr())
                 self.flag_ptr.append(self.flags.data_ptr())
                 self.out_ptr.append(self.out.data_ptr())
                 continue
@@ -136,10 +151,19 @@ class P2PAllReduce:
         dist.barrier(group=group)
 
     def _args(self, lo: int, hi: int, slot: int) -> P2PArgs:
+        """Kernel argument block of (lo, hi, slot), built once and cached (the host launch path is
+        on every eager step's critical path)."""
+        key = (lo, hi, slot)
+        a = self._arg_cache.get(key)
+        if a is None:
+            a = self._arg_cache[key] = self._make_args(lo, hi, slot)
+        return a
+
+    def _make_args(self, lo: int, hi: int, slot: int) -> P2PArgs:
         a = P2PArgs()
         a.out = self.out.data_ptr() + lo * 4
         for r in range(self.world):
-            a.inp[r] = self.in_ptr[r] + lo * 4
+            a.inp[r] = self.in_ptr[r] + lo * self.esize
             a.out_peer[r] = self.out_ptr[r] + lo * 4
             a.flags_peer[r] = self.flag_ptr[r]
         a.flags_local = self.flags.data_ptr()
@@ -154,33 +178,38 @@ class P2PAllReduce:
         return torch.cuda.current_stream().cuda_stream
 
     def begin_step(self):
-        """Before this step writes the gradient buffer: every peer finished reading it."""
+        """Before this step writes the gradient buffer: publish DONE for the previous step and
+        wait until every peer finished reading this rank's buffers (one launch)."""
         a = self._args(0, 4, 0)
-        _lib.check(self.L.drn_p2p_wait(ctypes.byref(a), ctypes.c_void_p(self.epoch.data_ptr()), self._stream()),
-                   "drn_p2p_wait")
+        _lib.check(self.L.drn_p2p_step(ctypes.byref(a), ctypes.c_void_p(self.epoch.data_ptr()), self._stream()),
+                   "drn_p2p_step")
 
     def reduce_bucket(self, i: int, lo: int, hi: int):
-        """Bucket i = grad[lo:hi] is complete on the current stream: publish it (compute stream)
-        and reduce it on the comm stream, whose kernel polls for the peers without blocking the
-        rest of this rank's backward pass."""
+        """Bucket i = grad[lo:hi] is complete on the current stream: (bf16 wire: cast it to the
+        shadow there) then ONE kernel on the comm stream publishes it, polls for the peers without
+        blocking the rest of this rank's backward pass, and reduces."""
         assert (hi - lo) % 4 == 0 and lo % 4 == 0 and i + 1 < N_SLOTS
         a = self._args(lo, hi, i + 1)
         cur = torch.cuda.current_stream()
-        _lib.check(self.L.drn_p2p_signal(ctypes.byref(a), 0, cur.cuda_stream), "drn_p2p_signal")
+        bf16 = self.shadow is not None
+        if bf16:
+            _lib.check(self.L.drn_p2p_cast(ctypes.c_void_p(self.grad.data_ptr() + lo * 4),
+                                           ctypes.c_void_p(self.shadow.data_ptr() + lo * 2), hi - lo,
+                                           cur.cuda_stream), "drn_p2p_cast")
         self.comm.wait_stream(cur)
         # at most 128 workgroups: a reduce waiting for a slow peer must leave most CUs to this
         # rank's own backward kernels (which publish the later buckets the peers wait for)
         blocks = max(1, min(128, (hi - lo) // 4 // 256))
         if (hi - lo) * 4 >= self.two_shot_min and self.world > 1:
-            _lib.check(self.L.drn_p2p_reduce2(ctypes.byref(a), blocks, self.comm.cuda_stream), "drn_p2p_reduce2")
+            _lib.check(self.L.drn_p2p_reduce2(ctypes.byref(a), blocks, int(bf16), self.comm.cuda_stream),
+                       "drn_p2p_reduce2")
         else:
-            _lib.check(self.L.drn_p2p_reduce(ctypes.byref(a), blocks, self.comm.cuda_stream), "drn_p2p_reduce")
+            _lib.check(self.L.drn_p2p_reduce(ctypes.byref(a), blocks, int(bf16), self.comm.cuda_stream),
+                       "drn_p2p_reduce")
 
     def end_step(self):
-        """All buckets reduced on this rank: tell the peers their inputs are free, and order the
-        compute stream after the reductions."""
-        a = self._args(0, 4, 0)
-        _lib.check(self.L.drn_p2p_signal(ctypes.byref(a), 1, self.comm.cuda_stream), "drn_p2p_signal")
+        """All buckets reduced on this rank: order the compute stream after the reductions (the
+        DONE publish happens at the next step's boundary launch)."""
         torch.cuda.current_stream().wait_stream(self.comm)
 
     def check(self):

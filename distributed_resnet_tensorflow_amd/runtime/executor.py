@@ -164,6 +164,11 @@ class Executor:
         assert policy in ("all", "1x1", "none"), policy
         self.bn_policy = policy
         self.materialize_bn = policy != "none"
+        # ... and (policy "1x1") BNs whose 1x1 consumer has >= DRN_BN_MAT_TILES 128-wide output-
+        # channel tiles: the fused prologue rewrites every input element once per output tile
+        # (and again in the weight gradient), so the bottleneck expansions (128->512, 256->1024,
+        # 512->2048: 4-16 tiles) spend more VALU on it than one streaming apply pass costs
+        self.mat_tiles = int(os.environ.get("DRN_BN_MAT_TILES", "100"))  # measured: 2 < 4 < 8 ~ off
         self.fdt = backend.acc_dtype
         self.P = params or ParamStore(spec, self.device, keep_bf16=self.is_hip, seed=seed, dtype=self.fdt)
         self.grad_ready: Optional[Callable[[int], None]] = None
@@ -378,7 +383,9 @@ class Executor:
         for bp in self.blocks:
             for i, b in enumerate(bp.bn):
                 consumers = [bp.convs[i].conv] + ([bp.proj.conv] if i == 0 and bp.proj is not None else [])
-                if self.bn_policy == "all" or (self.bn_policy == "1x1" and any(c.k != 1 for c in consumers)):
+                if self.bn_policy == "all" or (self.bn_policy == "1x1" and (
+                        any(c.k != 1 for c in consumers) or
+                        max(-(-c.cout // 128) for c in consumers) >= self.mat_tiles)):
                     b.act = self._act(*b.src.shape)
         for b in [b for bp in self.blocks for b in bp.bn] + [self.final_bn]:
             b.bacc, b.bG = self._stats_for(b.rows, b.bn.c)

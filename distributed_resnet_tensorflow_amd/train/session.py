@@ -45,7 +45,7 @@ def make_backend(device: str, precision: str = "bf16"):
 class TrainingSession:
     def __init__(self, spec, batch: int, cluster, *, weight_decay: float, lr_schedule, checkpoint_dir: str = "",
                  max_to_keep: int = 5, seed: int = 0, use_graph: bool = True, sync_mode: str = "sync",
-                 bucket_mb: float = 25.0, meta: Optional[dict] = None, allreduce: str = "rccl",
+                 bucket_mb: float = 25.0, meta: Optional[dict] = None, allreduce: str = "rccl", wire: str = "fp32",
                  collective_timeout_s: float = 0.0, precision: str = "bf16", shard_optimizer: bool = False):
         self.cluster = cluster
         self.spec = spec
@@ -54,7 +54,7 @@ class TrainingSession:
         self.ex = Executor(spec, batch, self.be, self.device, seed=seed, weight_decay=weight_decay)
         self.lr = lr_schedule
         self.meta = meta or {}
-        self.engine = DataParallelEngine(self.ex, bucket_mb=bucket_mb, mode=sync_mode, allreduce=allreduce,
+        self.engine = DataParallelEngine(self.ex, bucket_mb=bucket_mb, mode=sync_mode, allreduce=allreduce, wire=wire,
                                          timeout_s=collective_timeout_s,
                                          shard_optimizer=shard_optimizer) if cluster.distributed else None
         self.sharded = self.engine is not None and self.engine.zero1
@@ -72,11 +72,14 @@ class TrainingSession:
         self._restore()
         if self.device.type == "cuda" and self.be.name == "hip":
             self.ex.autotune()  # fix kernel configurations before any collective / graph capture
-        # one GPU: the whole step is one HIP graph. Data parallel: eager (measured faster than the
-        # chain of per-segment graphs, SegmentedStepGraph, which DRN_DP_GRAPH=1 selects)
+        # one GPU: the whole step is one HIP graph. Data parallel with the P2P all-reduce (every
+        # collective is a kernel with device-side flags): also the whole step, comm included, in
+        # one graph. Data parallel over RCCL: eager (measured faster than the chain
+        # of per-segment graphs, SegmentedStepGraph, which DRN_DP_GRAPH=1 selects)
+        dp_ok = cluster.distributed and self.engine.mode == "sync" and not self.sharded
         self.use_graph = use_graph and self.device.type == "cuda" and self.be.name == "hip" and (
-            not cluster.distributed or (os.environ.get("DRN_DP_GRAPH") == "1" and self.engine.p2p is None
-                                        and self.engine.mode == "sync" and not self.sharded))
+            not cluster.distributed or (dp_ok and self.engine.p2p is not None) or
+            (dp_ok and os.environ.get("DRN_DP_GRAPH") == "1"))
         if cluster.distributed and not self.use_graph and self.device.type == "cuda":
             from ..parallel.engine import use_priority_main_stream
             use_priority_main_stream()  # eager DP step: critical path on its own HW queue
@@ -134,7 +137,7 @@ class TrainingSession:
         self.ex.set_lr(self.cur_lr)
         if self.use_graph and not self.ex.check_nan:  # the debug checks synchronize: no capture
             if self._graph is None:  # warm-up = this real step
-                if self.engine is not None:
+                if self.engine is not None and self.engine.p2p is None:
                     self._graph = SegmentedStepGraph(self.ex, self.engine, 1.0 / self.world, warmup=1)
                 else:
                     self._graph = StepGraph(self._step_body, warmup=1)

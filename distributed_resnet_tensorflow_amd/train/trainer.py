@@ -105,7 +105,7 @@ def train(FLAGS, cluster=None):
     sess = TrainingSession(spec, FLAGS.batch_size, cluster, weight_decay=wd, lr_schedule=lr_mod.for_dataset(FLAGS.dataset),
                            checkpoint_dir=FLAGS.log_root, max_to_keep=FLAGS.max_to_keep, seed=FLAGS.seed,
                            use_graph=FLAGS.hip_graph, sync_mode=sync_mode, bucket_mb=FLAGS.bucket_mb,
-                           meta=_meta(FLAGS, spec), allreduce=FLAGS.allreduce,
+                           meta=_meta(FLAGS, spec), allreduce=FLAGS.allreduce, wire=FLAGS.allreduce_wire,
                            collective_timeout_s=FLAGS.collective_timeout_secs, precision=FLAGS.precision,
                            shard_optimizer=FLAGS.optimizer_sharding)
     feeder = make_feeder(FLAGS, sess.ex, cluster, True, sess.data_state)

@@ -23,7 +23,11 @@ def main():
     ap.add_argument("--sizes_kb", default="64,256,1024,4096,16384,65536")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--algos", default="rccl,p2p1,p2p2")
+    ap.add_argument("--algos", default="rccl,p2p1,p2p2,p2p1b,p2p2b",
+                    help="p2p1/p2p2: one-/two-shot fp32 wire; p2p1b/p2p2b: bf16 wire")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="also time the P2P step captured in a HIP graph (device-side latency, the way "
+                         "the training step runs it)")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -45,7 +49,8 @@ def main():
     algos = a.algos.split(",")
     if backend != "nccl":
         algos = [x for x in algos if x != "rccl"]
-    p2p = P2PAllReduce(grad) if any(x.startswith("p2p") for x in algos) else None
+    p2p = P2PAllReduce(grad) if any(x.startswith("p2p") and not x.endswith("b") for x in algos) else None
+    p2pb = P2PAllReduce(grad, wire="bf16") if any(x.startswith("p2p") and x.endswith("b") for x in algos) else None
 
     def fill(n):
         grad[:n].copy_(torch.arange(n, device="cuda", dtype=torch.float32).remainder_(97) + rank)
@@ -61,13 +66,14 @@ def main():
                     dist.all_reduce(grad[:n])
                 out = grad
             else:
-                p2p.two_shot_min = 0 if algo == "p2p2" else 1 << 62
+                pp = p2pb if algo.endswith("b") else p2p
+                pp.two_shot_min = 0 if algo.startswith("p2p2") else 1 << 62
 
-                def one():
-                    p2p.begin_step()
-                    p2p.reduce_bucket(0, 0, n)
-                    p2p.end_step()
-                out = p2p.out
+                def one(pp=pp):
+                    pp.begin_step()
+                    pp.reduce_bucket(0, 0, n)
+                    pp.end_step()
+                out = pp.out
             fill(n)
             one()
             torch.cuda.synchronize()
@@ -82,17 +88,38 @@ def main():
             torch.cuda.synchronize()
             dt = torch.tensor([(time.perf_counter() - t0) / a.iters], device="cuda")
             dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-            if p2p is not None:
-                p2p.check()
+            for pp in (p2p, p2pb):
+                if pp is not None:
+                    pp.check()
+            g_us = None
+            if a.graph and algo != "rccl":
+                # the same step captured in a HIP graph: what the data-parallel training step pays
+                g = torch.cuda.CUDAGraph()
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                torch.cuda.synchronize()
+                with torch.cuda.graph(g, stream=s):
+                    for _ in range(a.iters):
+                        one()
+                torch.cuda.synchronize()
+                dist.barrier()
+                t0 = time.perf_counter()
+                g.replay()
+                torch.cuda.synchronize()
+                gt = torch.tensor([(time.perf_counter() - t0) / a.iters], device="cuda")
+                dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+                g_us = round(float(gt.item()) * 1e6, 2)
+                ok = ok and bool(torch.allclose(out[:n], expected(n)))
             if rank == 0:
                 t = float(dt.item())
                 algbw = n * 4 / t / 1e9
                 print(json.dumps({"algo": algo, "bytes": n * 4, "world": world, "us": round(t * 1e6, 2),
-                                  "algbw_GBps": round(algbw, 2),
+                                  "graph_us": g_us, "algbw_GBps": round(algbw, 2),
                                   "busbw_GBps": round(algbw * 2 * (world - 1) / max(world, 1), 2), "correct": ok}),
                       flush=True)
-    if p2p is not None:
-        p2p.close()
+    for pp in (p2p, p2pb):
+        if pp is not None:
+            pp.close()
     dist.barrier()
     dist.destroy_process_group()
 

@@ -38,6 +38,9 @@ def _make(spec, N, shard, seed, be=None):
 def _worker(rank, world, port, q, allreduce="rccl"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        if allreduce.endswith("b"):      # bf16 gradients on the wire
+            os.environ["DRN_ALLREDUCE_WIRE"] = "bf16"
+            allreduce = allreduce[:-1]
         if allreduce == "p2p2":           # two-shot for every bucket
             os.environ["DRN_P2P_TWO_SHOT_MIN_KB"] = "0"
             allreduce = "p2p"
@@ -81,11 +84,12 @@ def _worker(rank, world, port, q, allreduce="rccl"):
         q.put((rank, repr(e) + traceback.format_exc(), False))
 
 
-@pytest.mark.parametrize("allreduce", ["rccl", "p2p", "p2p2"])
+@pytest.mark.parametrize("allreduce", ["rccl", "p2p", "p2p2", "rcclb", "p2pb", "p2p2b"])
 def test_dp_engine_gpu_two_ranks_one_device(allreduce):
     """rccl here means the engine's torch.distributed path (gloo on this one-GPU box); p2p is
     the one-shot HIP-IPC kernel path (parallel/p2p.py) with its device-side epoch flags, p2p2
-    its two-shot (reduce-scatter + all-gather) form."""
+    its two-shot (reduce-scatter + all-gather) form; a trailing b = bf16 gradients on the wire
+    (fp32 accumulation), whose rounding stays far inside the bf16-level tolerance below."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -175,3 +179,76 @@ def test_bench_multirank_code_path_one_device():
     assert len(lines) == 1, out.stdout
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["config"]["global_batch"] == 256 and r["value"] > 0
+
+
+def _graph_p2p_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DRN_DETERMINISTIC="1")
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2
+        from distributed_resnet_tensorflow_amd.ops.backend import HipBackend
+        from distributed_resnet_tensorflow_amd.parallel.engine import DataParallelEngine
+        from distributed_resnet_tensorflow_amd.runtime.graph import StepGraph
+        spec, N = cifar_resnet_v2(8), 8
+        be = HipBackend("cuda")                 # one backend: identical kernel configurations
+        exs, engs = [], []
+        for _ in range(2):
+            ex = _make(spec, N, rank, seed=1 + rank, be=be)
+            ex.set_lr(0.1)
+            eng = DataParallelEngine(ex, bucket_mb=0.05, allreduce="p2p")
+            assert eng.p2p is not None and len(eng.buckets) > 1
+            eng.broadcast_parameters()
+            exs.append(ex)
+            engs.append(eng)
+
+        def make_step(ex, eng):
+            def step():
+                ex.forward(True)
+                eng.begin_step()
+                ex.backward()
+                ex.apply_gradients(grad_scale=1.0 / world, grad=eng.finish())
+            return step
+
+        step_a, step_b = make_step(exs[0], engs[0]), make_step(exs[1], engs[1])
+        for _ in range(3):                      # eager reference: 3 data-parallel steps
+            step_a()
+        g = StepGraph(step_b, warmup=1)         # 1 eager warm-up step + the capture
+        g.replay()                              # ... + 2 replays = 3 steps
+        g.replay()
+        torch.cuda.synchronize()
+        for e in engs:
+            e.p2p.check()
+        bitwise = torch.equal(exs[0].P.master, exs[1].P.master) and torch.equal(exs[0].P.momentum,
+                                                                                 exs[1].P.momentum)
+        out = exs[1].P.master.double().sum().reshape(1).cpu()
+        gathered = [torch.zeros_like(out) for _ in range(world)]
+        dist.all_gather(gathered, out)
+        same = all(torch.equal(gathered[0], t) for t in gathered)
+        q.put((rank, bitwise, same))
+        dist.barrier()
+        for e in engs:
+            e.close()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), False))
+
+
+def test_graph_captured_dp_p2p_step_bitwise_equals_eager():
+    """the whole data-parallel step -- forward, backward with the side-stream
+    weight gradients, every bucket's P2P all-reduce (device-side epoch flags) and the fused SGD --
+    captured in ONE HIP graph and replayed is bitwise identical to the eager DP+P2P step
+    (deterministic mode: no atomics in the BN statistics), on two ranks sharing cuda:0."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_graph_p2p_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, bitwise, same in res:
+        assert bitwise is True, (rank, bitwise)
+        assert same
