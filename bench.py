@@ -203,7 +203,7 @@ def main():
     if os.environ.get("DRN_PRINT_TUNE") == "1" and rank == 0:
         for key, cfg, us in be.tune_log:
             print(f"[tune] {key} -> {cfg} ({us} us)", file=sys.stderr)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

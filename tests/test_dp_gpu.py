@@ -252,3 +252,60 @@ def test_graph_captured_dp_p2p_step_bitwise_equals_eager():
     for rank, bitwise, same in res:
         assert bitwise is True, (rank, bitwise)
         assert same
+
+
+def _schedule_worker(backend, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        torch.cuda.set_device(0)
+        kw = {"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}
+        dist.init_process_group(backend, rank=0, world_size=1, **kw)
+        from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2
+        from distributed_resnet_tensorflow_amd.parallel.engine import DataParallelEngine
+        spec, N = cifar_resnet_v2(20), 8
+        ex = _make(spec, N, 0, seed=1)
+        eng = DataParallelEngine(ex, bucket_mb=0.1)
+        log = []
+        launch = eng._launch
+
+        def rec(i, buf=None):
+            # (bucket, frontier when it fired, stream it was issued from)
+            side = ex.side is not None and torch.cuda.current_stream() == ex.side
+            log.append((i, eng.frontier, side))
+            return launch(i, buf)
+        eng._launch = rec
+        for _ in range(2):
+            ex.forward(True)
+            eng.begin_step()
+            ex.backward()
+            g = eng.finish()
+            ex.apply_gradients(grad_scale=1.0, grad=g)
+        torch.cuda.synchronize()
+        q.put((backend, log, [tuple(b) for b in eng.buckets], float(ex.P.grad.norm())))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((backend, repr(e) + traceback.format_exc(), None, None))
+
+
+def test_rccl_engine_bucket_schedule_matches_gloo():
+    """The RCCL (torch "nccl") engine issues the same buckets at the same backward positions, from
+    the weight-gradient side stream, as the gloo engine the multi-rank CPU/GPU rehearsals use: the
+    N>1 production path differs from the rehearsed one only in the transport."""
+    ctx = mp.get_context("spawn")
+    res = {}
+    for backend in ("nccl", "gloo"):
+        q = ctx.Queue()
+        p = ctx.Process(target=_schedule_worker, args=(backend, _free_port(), q))
+        p.start()
+        b, log, buckets, gn = q.get(timeout=300)
+        p.join(timeout=60)
+        assert isinstance(log, list), log
+        res[b] = (log, buckets, gn)
+    (ln, bn, gn_n), (lg, bg, gn_g) = res["nccl"], res["gloo"]
+    assert bn == bg and len(bn) > 2
+    assert ln == lg
+    assert len(ln) == 2 * len(bn)                      # every bucket once per step
+    assert all(side for _, _, side in ln[:-1])         # issued from the side stream (not the last,
+                                                       # which finish() issues on the main stream)
+    assert abs(gn_n - gn_g) <= 1e-3 * max(gn_g, 1e-6)
