@@ -169,6 +169,10 @@ class Executor:
         # (and again in the weight gradient), so the bottleneck expansions (128->512, 256->1024,
         # 512->2048: 4-16 tiles) spend more VALU on it than one streaming apply pass costs
         self.mat_tiles = int(os.environ.get("DRN_BN_MAT_TILES", "100"))  # measured: 2 < 4 < 8 ~ off
+        # ... but only BN tensors of >= DRN_BN_MAT_MIN_ELEMS elements: below that a step is
+        # launch-latency bound and the extra streaming launch costs more than the 3x3 consumer's
+        # in-LDS rewrite (CIFAR ResNet-50 bs 128: 2.45 ms materialised vs 2.33 ms fused)
+        self.mat_min_elems = int(os.environ.get("DRN_BN_MAT_MIN_ELEMS", str(4 << 20)))
         self.fdt = backend.acc_dtype
         self.P = params or ParamStore(spec, self.device, keep_bf16=self.is_hip, seed=seed, dtype=self.fdt)
         self.grad_ready: Optional[Callable[[int], None]] = None
@@ -383,7 +387,8 @@ class Executor:
         for bp in self.blocks:
             for i, b in enumerate(bp.bn):
                 consumers = [bp.convs[i].conv] + ([bp.proj.conv] if i == 0 and bp.proj is not None else [])
-                if self.bn_policy == "all" or (self.bn_policy == "1x1" and (
+                big = b.src.numel() >= self.mat_min_elems
+                if self.bn_policy == "all" or (self.bn_policy == "1x1" and big and (
                         any(c.k != 1 for c in consumers) or
                         max(-(-c.cout // 128) for c in consumers) >= self.mat_tiles)):
                     b.act = self._act(*b.src.shape)
