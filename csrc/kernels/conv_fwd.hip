@@ -514,16 +514,18 @@ __device__ __forceinline__ int glds_swz(int row) {
 // skipped and stay zero. The per-channel scale/shift are staged once into LDS behind the
 // pipeline stages. Used for 1x1 consumers, where it replaces a full streaming BN-apply pass.
 //
-// SROW: narrow-input convolutions (C == 8: the ImageNet 7x7/2 stem on RGB padded to 8 channels)
-// stage ONE FILTER ROW r per step: the 8 16-byte chunks of a 64-deep stage are the taps
-// s = 0..7 of that row (8 channels each; tap S..7 are zero-page pieces on both operands), so
+// SROW: narrow-input convolutions (C == 8: the ImageNet 7x7/2 stem on RGB padded to 8 channels;
+// C == 16: the CIFAR first stage) stage ONE FILTER ROW r per step: the 8 16-byte chunks of a
+// 64-deep stage are that row's S taps x C channels in KRSC / NHWC order (chunk lc = tap
+// lc*8/C, channels (lc*8)%C ..+7; chunks past S*C/8 are zero-page pieces on both operands), so
 // k = (r, s, c) keeps the reduction on the LDS-DMA path (per-lane pixel / tap validity) at
-// 8/7 of the 7x7x8 work instead of falling back to the register-staged kernel.
+// 64/(S*C) of the work instead of falling back to the register-staged kernel. With PRO the
+// fused BN prologue uses the lane's fixed chunk channel offset.
 template <int BP, int BC, int WAVES_P, int NS, int NW = 4, bool PF = true, int BK = 64, bool PRO = false,
           bool SROW = false>
 __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a, const void* __restrict__ zero) {
   static_assert(BK == 64 || BK == 32, "k per stage");
-  static_assert(!SROW || (BK == 64 && !PRO), "row-staged narrow convs: 64-deep stages, no fused prologue");
+  static_assert(!SROW || BK == 64, "row-staged narrow convs: 64-deep stages");
   constexpr int NT = NW * 64;
   constexpr int WAVES_C = NW / WAVES_P;
   constexpr int WP = BP / WAVES_P, WC = BC / WAVES_C;
@@ -595,17 +597,18 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
 
   auto issue = [&](int slot) {
     char* st = smem + slot * STAGE;
-    if constexpr (SROW) {  // stage = filter row ir; chunk lc = tap s
+    if constexpr (SROW) {  // stage = filter row ir; chunk lc = (tap lc*8/C, channels (lc*8)%C)
+      const int SC = a.S * C;
 #pragma unroll
       for (int i = 0; i < GA; ++i) {
-        const void* src = (wsrc[i] && alc[i] < a.S) ? (const void*)(wsrc[i] + (ir * a.S + alc[i]) * 8) : zero;
+        const void* src = (wsrc[i] && alc[i] * 8 < SC) ? (const void*)(wsrc[i] + ir * SC + alc[i] * 8) : zero;
         glds16(src, st + (RPG * NW * i + RPG * wave) * ROWB);
       }
 #pragma unroll
       for (int i = 0; i < GB; ++i) {
-        const int h = bh[i] + ir, w = bw[i] + blc[i];
-        const bool ok = blc[i] < a.S && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-        const void* src = ok ? (const void*)(xg + (boff[i] + (ir * a.W + blc[i]) * 8)) : zero;
+        const int h = bh[i] + ir, w = bw[i] + blc[i] * 8 / C;
+        const bool ok = blc[i] * 8 < SC && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+        const void* src = ok ? (const void*)(xg + (boff[i] + ir * a.W * C + blc[i] * 8)) : zero;
         glds16(src, st + (BC + RPG * NW * i + RPG * wave) * ROWB);
       }
       ++ir;
@@ -688,7 +691,8 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
     if constexpr (PRO) {
       char* sw = smem + (t % NS) * STAGE;
       // one LDS round trip: this stage's scale/shift and the lane's landed pieces together
-      const uint32_t sp = lds_addr(ssl + xci + lcb * 8);
+      // (SROW: the lane's chunk maps to a fixed tap / channel group in every stage)
+      const uint32_t sp = lds_addr(ssl + (SROW ? (lcb * 8) % C : xci + lcb * 8));
       u32x4_t v[GB + 4];
       v[GB] = lds_read16(sp);
       v[GB + 1] = lds_read16(sp + 16);
@@ -697,8 +701,9 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
       uint32_t pa[GB], ok = 0;
 #pragma unroll
       for (int i = 0; i < GB; ++i) {
-        const int h = bh[i] + xr, w = bw[i] + xs;
-        ok |= ((unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) ? (1u << i) : 0u;
+        const int h = bh[i] + xr, w = bw[i] + (SROW ? lcb * 8 / C : xs);
+        const bool chunk_ok = !SROW || lcb * 8 < a.S * C;
+        ok |= (chunk_ok && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) ? (1u << i) : 0u;
         pa[i] = lds_addr(sw + (BC + RPG * NW * i + RPG * wave) * ROWB + lane * 16);
         v[i] = lds_read16(pa[i]);
       }
@@ -712,8 +717,9 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
         sh2[2 * q + 1] = f32x2_t{__uint_as_float(v[GB + 2 + q][2]), __uint_as_float(v[GB + 2 + q][3])};
       }
       lds_bn_relu_store<GB, true>(pa, v, ok, sc2, sh2);
-      xci += BK;
-      if (xci == C) {
+      if (SROW) {
+        ++xr;
+      } else if ((xci += BK) == C) {
         xci = 0;
         if (++xs == a.S) {
           xs = 0;
@@ -792,9 +798,12 @@ static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t 
 template <int BP, int BC, int WAVES_P, int NS, int NW = 4, int BK = 64>
 static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
   const bool pf = a->residual != nullptr || a->bn_x != nullptr;
-  if (a->C == 8) {  // row-staged narrow conv (the stem)
+  if (a->C == 8 || a->C == 16) {  // row-staged narrow conv (the stem, the CIFAR first stage)
     if constexpr (BK == 64) {
-      if (a->S > 8 || a->in_scale != nullptr) return (int)hipErrorInvalidValue;
+      if (a->S * a->C > 64) return (int)hipErrorInvalidValue;
+      if (a->in_scale != nullptr)
+        return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, true, true>(a, zero, stream)
+                  : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, true, true>(a, zero, stream);
       return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, false, true>(a, zero, stream)
                 : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false, true>(a, zero, stream);
     }
@@ -833,7 +842,9 @@ static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t str
   X(19, 128, 64, 2, 4, 4, 32)  \
   X(20, 128, 128, 2, 3, 4, 32) \
   X(21, 64, 128, 1, 3, 4, 32)  \
-  X(22, 256, 64, 4, 4, 4, 32)
+  X(22, 256, 64, 4, 4, 4, 32)  \
+  X(23, 256, 32, 4, 2, 4)      \
+  X(24, 128, 32, 4, 3, 4)
 
 static int launch_glds_cfg(int cfg, DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
   switch (cfg) {
@@ -864,7 +875,7 @@ static int glds_cfg_bp(int cfg) {
 // 64 x 128 tiles once the 128 x 128 grid stops filling the chip.
 static int glds_default_cfg(const DrnConvFwdArgs* a) {
   const long M = (long)a->N * a->P * a->Q;
-  if (a->C == 8) return a->K <= 64 ? 3 : 0;  // row-staged narrow conv: 64-deep stages only
+  if (a->C == 8 || a->C == 16) return a->K <= 32 ? 23 : a->K <= 64 ? 3 : 0;  // row-staged: 64-deep stages
   if (a->C % 64) return 18;  // 32-channel inputs: the 32-deep-stage family
   auto blocks = [&](int bp, int bc) { return ((M + bp - 1) / bp) * ((a->K + bc - 1) / bc); };
   if (a->K <= 64) return blocks(256, 64) >= 384 ? 3 : 7;
@@ -910,8 +921,8 @@ DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s);
 
 // Whether the LDS-DMA kernel family supports this convolution.
 DRN_API int drn_conv_glds_ok(const DrnConvFwdArgs* a) {
-  if (a->C == 8)  // row-staged narrow conv (stem): no fused BN prologue
-    return a->dil == 1 && a->S <= 8 && a->in_scale == nullptr;
+  if (a->C == 8 || a->C == 16)  // row-staged narrow conv (stem, CIFAR stage 1)
+    return a->dil == 1 && a->S * a->C <= 64 && (a->in_scale == nullptr || a->relu_in != 0);
   return a->C % 32 == 0 && a->dil == 1 && (a->in_scale == nullptr || (a->C <= 4096 && a->relu_in != 0));
 }
 
@@ -939,7 +950,7 @@ DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
 }
 
 DRN_API int drn_conv_glds_cfg_bp(int cfg) { return drn::glds_cfg_bp(cfg); }
-DRN_API int drn_conv_glds_num_cfgs() { return 23; }
+DRN_API int drn_conv_glds_num_cfgs() { return 25; }
 DRN_API int drn_conv_glds_default_cfg(const DrnConvFwdArgs* a) { return drn::glds_default_cfg(a); }
 
 DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s) {

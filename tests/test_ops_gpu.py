@@ -83,11 +83,14 @@ GLDS_CASES = [
     (2, 9, 9, 96, 64, 3, 1, 1),        # C % 64 != 0: only the 32-deep-stage configs apply
     (2, 16, 16, 8, 64, 7, 2, 3),       # C == 8 (stem): row-staged, 64-deep-stage configs only
     (2, 9, 9, 8, 16, 3, 1, 1),         # C == 8, 3x3 (taps 3..7 of each stage are zero pieces)
+    (2, 10, 10, 16, 16, 3, 1, 1),      # C == 16 (CIFAR stage 1): 2 chunks per tap, chunks 6, 7 zero
+    (2, 9, 9, 16, 32, 3, 2, 1),        # C == 16, stride 2
+    (2, 8, 8, 16, 64, 1, 1, 0),        # C == 16, 1x1 (chunks 2..7 zero)
 ]
 
 
 @pytest.mark.parametrize("case", GLDS_CASES)
-@pytest.mark.parametrize("cfg", list(range(23)))
+@pytest.mark.parametrize("cfg", list(range(25)))
 @pytest.mark.parametrize("pro", [False, True])
 def test_conv_fwd_glds_configs(hip, ref, case, cfg, pro):
     """Every tile/pipeline configuration of the LDS-DMA conv kernel vs the fp32 reference,
@@ -100,8 +103,6 @@ def test_conv_fwd_glds_configs(hip, ref, case, cfg, pro):
     w = bf(torch.randn(K, R, R, C) * (2.0 / (R * R * C)) ** 0.5)
     res = bf(torch.randn(N, P, P, K))
     g = ConvGeom(stride=s, pad_h=p, pad_w=p)
-    if pro and C == 8:
-        pytest.skip("the row-staged narrow conv has no fused prologue")
     in_bn = (torch.rand(C) + 0.5, torch.randn(C) * 0.5) if pro else None
     y_ref = torch.zeros(N, P, P, K)
     st_ref = torch.zeros(2 * K)
@@ -112,7 +113,8 @@ def test_conv_fwd_glds_configs(hip, ref, case, cfg, pro):
                       in_bn=None if in_bn is None else (in_bn[0].cuda(), in_bn[1].cuda()))
     assert hip.L.drn_conv_glds_ok(a) == 1 and a.stats_rep == 3
     a.cfg = cfg
-    if (C % 64 and C != 8 and cfg < 17) or (C == 8 and cfg >= 17):
+    narrow = C in (8, 16)                # row-staged: the 64-deep-stage configurations only
+    if (C % 64 and not narrow and (cfg < 17 or cfg > 22)) or (narrow and 17 <= cfg <= 22):
         assert hip.L.drn_conv_fwd2(ctypes.byref(a), hip.zero_page.data_ptr(), hip.stream()) != 0
         return
     hip.launch_conv(a)
