@@ -26,6 +26,38 @@
 
 namespace drn {
 
+// Optional per-workgroup timeline of the LDS-DMA conv kernel (diagnostics only; null in normal
+// runs): record b = {start, main-loop end, end} in s_memrealtime ticks (100 MHz) + HW_ID / XCC_ID.
+__device__ unsigned long long* g_conv_trace = nullptr;
+
+__device__ __forceinline__ unsigned long long drn_realtime() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
+  return t;
+}
+
+// Sum of x over the lanes of a wave that are congruent mod CHR (CHR = 2..32, a power of two):
+// row rotations by CHR, 2*CHR .. 8 inside each 16-lane DPP row, then the cross-row partners via
+// v_permlane16_swap (lane ^ 16) and v_permlane32_swap (lane ^ 32). Every such lane gets the sum.
+template <int S>
+__device__ __forceinline__ float dpp_row_ror(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x120 | S, 0xF, 0xF, false));
+}
+
+template <int CHR>
+__device__ __forceinline__ float chunk_lane_sum(float x) {
+  static_assert(CHR >= 2 && CHR <= 32 && (CHR & (CHR - 1)) == 0, "chunk count");
+  if constexpr (CHR <= 2) x += dpp_row_ror<2>(x);
+  if constexpr (CHR <= 4) x += dpp_row_ror<4>(x);
+  if constexpr (CHR <= 8) x += dpp_row_ror<8>(x);
+  if constexpr (CHR <= 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // ---------------- shared epilogue ----------------
 // Every lane owns 8 consecutive channels (one 16-byte bf16 chunk) of BP/RPI pixel rows.
 // epi_prefetch() computes those output offsets and issues the 16-byte loads of the residual
@@ -241,20 +273,32 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
     }
   }
   if (want_stats) {
-    __syncthreads();
-    float* red = tile;  // [NT][17]: row stride 17 floats keeps the per-j column writes and the
-                        // strided reads bank-conflict free (stride 16 was a 16-way conflict)
+    // (1) within the wave: the lanes holding the same 8-channel chunk are lane = ch (mod CHR);
+    //     DPP row rotations inside each 16-lane row, then permlane16/32 swaps across rows
+    float v[16];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      red[tid * 17 + j] = ssum[j];
-      red[tid * 17 + 8 + j] = ssq[j];
+      v[j] = chunk_lane_sum<CHR>(ssum[j]);
+      v[8 + j] = chunk_lane_sum<CHR>(ssq[j]);
+    }
+    // (2) across the waves through LDS: [wave][chunk][16] wave totals
+    constexpr int NWV = NT / 64;
+    __syncthreads();  // every thread is done reading the staged tile
+    float* red = tile;
+    const int wv = tid >> 6, ln = tid & 63;
+    if (ln < CHR) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<float4*>(red + (wv * CHR + ln) * 16 + 4 * q) =
+            make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
     }
     __syncthreads();
     for (int t = tid; t < 2 * BC; t += NT) {  // 2*BC may exceed the thread count (BC = 256)
       const int cl = t >> 1, which = t & 1;
       const int chh = cl >> 3, j = cl & 7;
       float s = 0.f;
-      for (int t2 = chh; t2 < NT; t2 += CHR) s += red[t2 * 17 + which * 8 + j];
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) s += red[(w * CHR + chh) * 16 + which * 8 + j];
       const int rep = a.stats_rep > 1 ? a.stats_rep : 1;
       if (c0 + cl < a.K) atomicAdd(a.stats + ((size_t)(blockIdx.x % rep) * 2 + which) * a.K + c0 + cl, s);
     }
@@ -543,6 +587,9 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
 
   extern __shared__ __attribute__((aligned(1024))) char smem[];
 
+  unsigned long long* const trace = g_conv_trace;
+  unsigned long long t_start = 0;
+  if (trace != nullptr) t_start = drn_realtime();
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -658,7 +705,9 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   const int T = SROW ? a.R : Ktot / BK;
   // fused-BN operands: [scale C][shift C] fp32 behind the stages, written AFTER the first
   // pipeline stages are issued (their LDS-DMA latency covers the parameter loads / finalize)
-  float* const ssl = reinterpret_cast<float*>(smem + NS * STAGE);
+  // (behind the stages actually used: a convolution with fewer k-stages than NS - e.g. a 1x1
+  // over 64 channels, T = 1 - gets only T stage slots, so more workgroups fit a CU)
+  float* const ssl = reinterpret_cast<float*>(smem + (T < NS ? T : NS) * STAGE);
   // the lane's logical 16-byte chunk of the B rows it loads: identical for every piece i
   // (RPG * NW rows apart leave the swizzle bits unchanged)
   static_assert((RPG * NW) % 16 == 0, "piece stride must preserve the swizzle bits");
@@ -748,8 +797,23 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
     asm volatile("" ::: "memory");
   }
   __syncthreads();  // all fragment reads done before the epilogue reuses the LDS
+  unsigned long long t_loop = 0;
+  if (trace != nullptr) t_loop = drn_realtime();
   // (the launcher sizes the dynamic LDS for max(NS * STAGE, BP * BC * 4))
   conv_epilogue<BP, BC, WP, WC, MI, MJ, NT, PF>(a, smem, acc, wp, wc, m0, c0, M, epre);
+  if (trace != nullptr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+      unsigned long long* r = trace + 4 * (size_t)blockIdx.x;
+      r[0] = t_start;
+      r[1] = t_loop;
+      r[2] = drn_realtime();
+      r[3] = ((unsigned long long)xcc << 32) | hw;
+    }
+  }
 }
 
 // largest grid that finalizes its input BatchNorm in the prologue (DRN_CFIN_MAX_BLOCKS)
@@ -764,7 +828,8 @@ static int cfin_max_blocks() {
 
 template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF, int BK, bool PRO, bool SROW = false>
 static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
-  constexpr int LDS0 = NS * (BC + BP) * BK * 2;
+  const int T = a->C == 8 || a->C == 16 ? a->R : (a->R * a->S * a->C) / BK;  // k-stages (SROW: filter rows)
+  const int LDS0 = (T < NS ? T : NS) * (BC + BP) * BK * 2;         // stage slots actually used
   const int lds_main = LDS0 + (PRO ? 8 * a->C : 0);                 // + fused-BN scale/shift
   const int LDS = lds_main > BP * BC * 4 ? lds_main : BP * BC * 4;  // epilogue staging tile
   if (LDS > 160 * 1024) return (int)hipErrorInvalidValue;
@@ -919,6 +984,12 @@ DRN_API int drn_conv_fwd_tiles_p(int M, int K) {
 
 DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s);
 
+// multi-tile LDS-DMA family (conv_mt.hip): config ids DRN_GLDS_NCFG .. + drn_conv_mt_num_cfgs()
+DRN_API int drn_conv_mt(int cfg, DrnConvFwdArgs* a, const void* zero, hipStream_t s);
+DRN_API int drn_conv_mt_num_cfgs();
+DRN_API int drn_conv_mt_ok(const DrnConvFwdArgs* a);
+#define DRN_GLDS_NCFG 25
+
 // Whether the LDS-DMA kernel family supports this convolution.
 DRN_API int drn_conv_glds_ok(const DrnConvFwdArgs* a) {
   if (a->C == 8 || a->C == 16)  // row-staged narrow conv (stem, CIFAR stage 1)
@@ -935,6 +1006,7 @@ DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
   if (a->in_fin.stats != nullptr &&
       (a->in_scale == nullptr || a->in_fin.C != a->C || a->in_fin.G < 1 || a->in_fin.G > DRN_BN_FIN_GMAX))
     return (int)hipErrorInvalidValue;
+  if (a->cfg >= DRN_GLDS_NCFG && a->cfg != 100) return drn_conv_mt(a->cfg - DRN_GLDS_NCFG, a, zero, s);
   if (drn_conv_glds_ok(a) && zero != nullptr && a->cfg != 100)
     return drn::launch_glds_cfg(a->cfg >= 0 ? a->cfg : drn::glds_default_cfg(a), a, zero, s);
   if (a->in_fin.stats != nullptr) {
@@ -949,8 +1021,13 @@ DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
   return drn_conv_fwd(a, s);
 }
 
+// diagnostics: per-workgroup timeline buffer for the LDS-DMA conv kernel (nullptr disables)
+DRN_API int drn_conv_trace_set(unsigned long long* buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(drn::g_conv_trace), &buf, sizeof(buf));
+}
+
 DRN_API int drn_conv_glds_cfg_bp(int cfg) { return drn::glds_cfg_bp(cfg); }
-DRN_API int drn_conv_glds_num_cfgs() { return 25; }
+DRN_API int drn_conv_glds_num_cfgs() { return DRN_GLDS_NCFG + drn_conv_mt_num_cfgs(); }
 DRN_API int drn_conv_glds_default_cfg(const DrnConvFwdArgs* a) { return drn::glds_default_cfg(a); }
 
 DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s) {

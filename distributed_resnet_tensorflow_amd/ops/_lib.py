@@ -80,6 +80,7 @@ _SIGS = {
     "drn_conv_fwd2": ([ctypes.POINTER(DrnConvFwdArgs), c_p, c_p], c_int),
     "drn_conv_glds_ok": ([ctypes.POINTER(DrnConvFwdArgs)], c_int),
     "drn_conv_glds_num_cfgs": ([], c_int),
+    "drn_conv_trace_set": ([c_p], c_int),
     "drn_conv_glds_default_cfg": ([ctypes.POINTER(DrnConvFwdArgs)], c_int),
     "drn_conv_wgrad": ([ctypes.POINTER(DrnConvWgradArgs), c_p], c_int),
     "drn_conv_wgrad2": ([ctypes.POINTER(DrnConvWgradArgs), c_p, c_int, c_p], c_int),

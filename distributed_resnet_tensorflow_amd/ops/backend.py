@@ -380,13 +380,18 @@ class HipBackend(_Common):
         splits = (steps + per - 1) // per
         return splits, per * 64
 
-    def wgrad_args(self, x, dy, out, g: ConvGeom, in_bn=None, relu_in=True, ws=None):
+    # split-K block targets the wgrad autotuner chooses from per geometry: more splits fill the
+    # chip, fewer write (and re-read in drn_splitk_reduce) fewer fp32 partial slabs -- the slab
+    # traffic of the default 512-block target is ~1.7 GB per ResNet-50 step
+    WGRAD_TARGETS = tuple(int(v) for v in os.environ.get("DRN_WGRAD_TARGETS", "128,256,512").split(","))
+
+    def wgrad_args(self, x, dy, out, g: ConvGeom, in_bn=None, relu_in=True, ws=None, target_blocks: int = 0):
         N, H, W, C = x.shape
         N2, P, Q, K = dy.shape
         Kd, R, S, Cd = out.shape
         assert Kd == K and Cd == C and N == N2
         M = N * P * Q
-        splits, pps = self.wgrad_splits(M, R * S * C, K)
+        splits, pps = self.wgrad_splits(M, R * S * C, K, target_blocks)
         a = _lib.DrnConvWgradArgs()
         a.x, a.dy = x.data_ptr(), dy.data_ptr()
         a.in_scale = _ptr(in_bn[0]) if in_bn is not None else None
@@ -406,55 +411,70 @@ class HipBackend(_Common):
         return a
 
     def wgrad_ws_elems(self, M, K, R, S, C):
-        splits, _ = self.wgrad_splits(M, R * S * C, K)
-        return splits * K * R * S * C if splits > 1 else 0
+        """Workspace for the largest split count any candidate target can choose."""
+        need = 0
+        for t in set(self.WGRAD_TARGETS) | {self.WGRAD_TARGET_BLOCKS}:
+            splits, _ = self.wgrad_splits(M, R * S * C, K, t)
+            if splits > 1:
+                need = max(need, splits * K * R * S * C)
+        return need
 
     @staticmethod
     def wgrad_key(a) -> tuple:
-        return (a.N, a.H, a.W, a.C, a.K, a.R, a.S, a.P, a.Q, a.stride, a.pad_h, a.pad_w,
-                a.in_scale is not None, a.splits)
+        return (a.N, a.H, a.W, a.C, a.K, a.R, a.S, a.P, a.Q, a.stride, a.pad_h, a.pad_w, a.in_scale is not None)
 
     def _wgrad_kernel(self, a, ns: int, st):
         _lib.check(self.L.drn_conv_wgrad2(ctypes.byref(a), self.zero_page.data_ptr(), ns, st), "drn_conv_wgrad")
 
-    def _tune_wgrad(self, a, key, iters: int = 5) -> int:
-        """Pick the wgrad pipeline (0: register-staged, 2/3: LDS-DMA stages of 64 pixels, 4/5/6:
-        2/3/4 stages of 32 pixels) by timing; the
-        kernel only writes the split-K workspace (or the gradient slot, rewritten right after)."""
-        st = self.stream()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        best, best_t = 2, float("inf")
-        cands = tuple(int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6").split(","))
-        for ns in cands:
-            for _ in range(2):
-                self._wgrad_kernel(a, ns, st)
-            ev0.record()
-            for _ in range(iters):
-                self._wgrad_kernel(a, ns, st)
-            ev1.record()
-            ev1.synchronize()
-            ms = ev0.elapsed_time(ev1) / iters
-            if ms < best_t:
-                best, best_t = ns, ms
-        self.tune_log.append((("wgrad",) + key, best, round(best_t * 1e3, 1)))
-        return best
-
-    def launch_wgrad(self, a, out):
-        st = self.stream()
-        if self.forced_wgrad_ns is not None:
-            ns = self.forced_wgrad_ns
-        else:
-            key = self.wgrad_key(a)
-            if key not in self.wgrad_ns and self.autotune and not torch.cuda.is_current_stream_capturing():
-                self.wgrad_ns[key] = self._tune_wgrad(a, key)
-            ns = self.wgrad_ns.get(key, 2)
+    def _wgrad_full(self, a, ns: int, out, st):
         self._wgrad_kernel(a, ns, st)
         if a.splits > 1:
             _lib.check(self.L.drn_splitk_reduce(a.out, out.data_ptr(), out.numel(), a.splits, 1.0, 0, st),
                        "drn_splitk_reduce")
 
+    def _tune_wgrad(self, args_for, out, key, iters: int = 5) -> tuple:
+        """Pick (split-K target, pipeline) by timing the weight-gradient kernel TOGETHER with its
+        split-K reduction: 0 = register-staged, 2/3 = LDS-DMA stages of 64 pixels, 4/5/6 = 2/3/4
+        stages of 32 pixels. Writes only the workspace and this gradient slot (rewritten by the
+        real launch that follows)."""
+        st = self.stream()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        best, best_t = (0, 2), float("inf")
+        cands = tuple(int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6").split(","))
+        seen = set()
+        for tgt in self.WGRAD_TARGETS:
+            a = args_for(tgt)
+            if a.splits in seen:
+                continue
+            seen.add(a.splits)
+            for ns in cands:
+                for _ in range(2):
+                    self._wgrad_full(a, ns, out, st)
+                ev0.record()
+                for _ in range(iters):
+                    self._wgrad_full(a, ns, out, st)
+                ev1.record()
+                ev1.synchronize()
+                ms = ev0.elapsed_time(ev1) / iters
+                if ms < best_t:
+                    best, best_t = (tgt, ns), ms
+        self.tune_log.append((("wgrad",) + key, best, round(best_t * 1e3, 1)))
+        return best
+
     def conv_wgrad(self, x, dy, out, g, in_bn=None, relu_in=True, ws=None):
-        self.launch_wgrad(self.wgrad_args(x, dy, out, g, in_bn, relu_in, ws), out)
+        args_for = lambda tgt: self.wgrad_args(x, dy, out, g, in_bn, relu_in, ws, tgt)
+        a = args_for(0)
+        st = self.stream()
+        if self.forced_wgrad_ns is not None:
+            self._wgrad_full(a, self.forced_wgrad_ns, out, st)
+            return
+        key = self.wgrad_key(a)
+        if key not in self.wgrad_ns and self.autotune and not torch.cuda.is_current_stream_capturing():
+            self.wgrad_ns[key] = self._tune_wgrad(args_for, out, key)
+        tgt, ns = self.wgrad_ns.get(key, (0, 2))
+        if tgt:
+            a = args_for(tgt)
+        self._wgrad_full(a, ns, out, st)
 
     # -- batch norm -----------------------------------------------------------------------------
     @staticmethod
