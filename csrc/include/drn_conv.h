@@ -179,6 +179,12 @@ struct DrnConvFwdArgs {
   // prologue): when in_fin.stats is set the prologue derives scale/shift from the statistics
   // instead of reading in_scale/in_shift (see DrnBnFin).
   DrnBnFin in_fin;
+  // Optional fused BatchNorm-backward input (data gradients, LDS-DMA kernels): the conv input
+  // dY is dx of a BatchNorm whose apply was not materialised, dY = A*x + B*bnb_x + D per
+  // channel with (A, B, D) finalized from bnb_fin's backward statistics (drn_bn_fin_bwd);
+  // x holds the ReLU-masked gradient g, bnb_x the BatchNorm's input.
+  const void* bnb_x;
+  DrnBnFin bnb_fin;
 };
 
 // dW[K][R][S][C] (+)= sum_{n,p,q} dy[n,p,q,k] * x[n, p*st-pad+r, q*st-pad+s, c]
@@ -195,4 +201,7 @@ struct DrnConvWgradArgs {
   int32_t relu_in;
   int32_t splits, pix_per_split;
   DrnFastDiv fd_pq, fd_q;
+  // Optional fused BatchNorm-backward dY (see DrnConvFwdArgs::bnb_x): dY_eff = A*dy + B*bnb_x + D
+  const void* bnb_x;
+  DrnBnFin bnb_fin;
 };

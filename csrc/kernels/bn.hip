@@ -726,6 +726,7 @@ DRN_API int drn_bn_bwd_apply_fin(const void* dy, const float* dpool, int pool_hw
 
 DRN_API int drn_bn_fin_size() { return (int)sizeof(DrnBnFin); }
 DRN_API int drn_conv_args_size() { return (int)sizeof(DrnConvFwdArgs); }
+DRN_API int drn_wgrad_args_size() { return (int)sizeof(DrnConvWgradArgs); }
 
 DRN_API int drn_bn_bwd_apply(const void* dy, const float* dpool, int pool_hw, const void* x, const float* scale,
                              const float* shift, const float* mean, const float* invstd, const float* coef,

@@ -30,6 +30,13 @@ namespace drn {
 // runs): record b = {start, main-loop end, end} in s_memrealtime ticks (100 MHz) + HW_ID / XCC_ID.
 __device__ unsigned long long* g_conv_trace = nullptr;
 
+// Cache-policy switch of the conv epilogue (drn_conv_set_flags): bit 0 = nontemporal output
+// stores. Measured per conv in isolation 2-5 % faster (scripts/nt_ab.py: the once-written output
+// stays out of the L2 holding the k-loop's operand reuse), but no faster in the full step, where
+// the next layer reads that output; default off. Nontemporal LDS-DMA of the reused operands
+// was slower everywhere.
+__device__ int g_conv_flags = 0;
+
 __device__ __forceinline__ unsigned long long drn_realtime() {
   unsigned long long t;
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
@@ -246,7 +253,12 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
         }
         *reinterpret_cast<uint4*>(y + off) = pack8(f);
       } else {
-        *reinterpret_cast<uint4*>(y + off) = o;
+        if (g_conv_flags & 1) {
+          const u32x4_t ov = {o.x, o.y, o.z, o.w};
+          __builtin_nontemporal_store(ov, reinterpret_cast<u32x4_t*>(y + off));
+        } else {
+          *reinterpret_cast<uint4*>(y + off) = o;
+        }
         if (a.out_fill && a.out_stride > 1) {
           // zeros at this pixel's sibling phase positions (single-phase strided output)
           const int m = m0 + row;
@@ -534,6 +546,7 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_base) {
   __builtin_amdgcn_global_load_lds((drn_gbl_void*)src, (drn_lds_void*)lds_base, 16, 0, 0);
 }
 
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -565,11 +578,21 @@ __device__ __forceinline__ int glds_swz(int row) {
 // k = (r, s, c) keeps the reduction on the LDS-DMA path (per-lane pixel / tap validity) at
 // 64/(S*C) of the work instead of falling back to the register-staged kernel. With PRO the
 // fused BN prologue uses the lane's fixed chunk channel offset.
+//
+// BNB: the input dY of this (data-gradient) convolution is the output of a BatchNorm backward
+// that is NOT materialised: dY = A[c] * g + B[c] * x + D[c] (dx = gamma*invstd * (g - mean g -
+// xhat * mean(g*xhat)) folded per channel, drn_bn_fin_bwd), with g = a.x the ReLU-masked
+// gradient and x = a.bnb_x the BatchNorm's input. Each stage DMAs the x pieces next to the g
+// pieces ([A rows][B rows][X rows]); after the counted vmcnt wait every lane rewrites its own
+// landed g pieces in place (the same one-LDS-round-trip scheme as PRO), zero pieces stay zero.
+// The coefficients come from the BN statistics replicas in the prologue (consumer-side
+// finalize; the first workgroup of the publishing launch writes dgamma / dbeta).
 template <int BP, int BC, int WAVES_P, int NS, int NW = 4, bool PF = true, int BK = 64, bool PRO = false,
-          bool SROW = false>
+          bool SROW = false, bool BNB = false>
 __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a, const void* __restrict__ zero) {
   static_assert(BK == 64 || BK == 32, "k per stage");
   static_assert(!SROW || BK == 64, "row-staged narrow convs: 64-deep stages");
+  static_assert(!(BNB && (PRO || SROW)), "one input transform per launch");
   constexpr int NT = NW * 64;
   constexpr int WAVES_C = NW / WAVES_P;
   constexpr int WP = BP / WAVES_P, WC = BC / WAVES_C;
@@ -577,9 +600,9 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   constexpr int ROWB = BK * 2;              // bytes of one LDS row (BK bf16 of k)
   constexpr int CPR = BK / 8;               // 16-byte chunks per row
   constexpr int RPG = 1024 / ROWB;          // rows per glds wave-instruction (1 KiB)
-  constexpr int STAGE = (BC + BP) * ROWB;
+  constexpr int STAGE = (BC + BP * (BNB ? 2 : 1)) * ROWB;
   constexpr int GA = BC / (RPG * NW), GB = BP / (RPG * NW);  // glds wave-instructions per stage
-  constexpr int G = GA + GB;
+  constexpr int G = GA + GB * (BNB ? 2 : 1);
   constexpr int D = NS - 1;                 // stages in flight ahead of the computing one
   static_assert(WAVES_P * WAVES_C == NW && MI >= 1 && MJ >= 1, "wave layout");
   static_assert(GA * RPG * NW == BC && GB * RPG * NW == BP, "rows must split evenly over the waves");
@@ -674,6 +697,16 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
       const void* src = ok ? (const void*)(xg + (boff[i] + tap_off)) : zero;
       glds16(src, st + (BC + RPG * NW * i + RPG * wave) * ROWB);
     }
+    if constexpr (BNB) {  // the BatchNorm input pieces at the same positions
+      const bf16_t* __restrict__ bx = reinterpret_cast<const bf16_t*>(a.bnb_x);
+#pragma unroll
+      for (int i = 0; i < GB; ++i) {
+        const int h = bh[i] + ir, w = bw[i] + is;
+        const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+        const void* src = ok ? (const void*)(bx + (boff[i] + tap_off)) : zero;
+        glds16(src, st + (BC + BP + RPG * NW * i + RPG * wave) * ROWB);
+      }
+    }
     ik += BK;
     ici += BK;
     if (ici == C) {
@@ -732,11 +765,67 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
     }
     __syncthreads();
   }
+  if constexpr (BNB) {
+    // consumer-side BN-backward finalize: dY = A*g + B*x + D per channel, [A C][B C][D C]
+    const bool pub = a.bnb_fin.publish && blockIdx.x == 0;
+    for (int c = tid; c < C; c += NT) drn_bn_fin_bwd(a.bnb_fin, c, pub, ssl[c], ssl[C + c], ssl[2 * C + c]);
+    __syncthreads();
+  }
 
   for (int t = 0; t < T; ++t) {
     // retire stage t: the stages issued after it (up to D-1) may stay in flight
     if (t + D - 1 < T) wait_vmcnt<G * (D - 1)>();
     else wait_vmcnt<0>();
+    if constexpr (BNB) {
+      char* sw = smem + (t % NS) * STAGE;
+      const uint32_t sp = lds_addr(ssl + xci + lcb * 8);
+      u32x4_t v[2 * GB + 6];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        v[2 * GB + 2 * q] = lds_read16(sp + 4 * q * C);
+        v[2 * GB + 2 * q + 1] = lds_read16(sp + 4 * q * C + 16);
+      }
+      uint32_t pa[GB], ok = 0;
+#pragma unroll
+      for (int i = 0; i < GB; ++i) {
+        const int h = bh[i] + xr, w = bw[i] + xs;
+        ok |= ((unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) ? (1u << i) : 0u;
+        pa[i] = lds_addr(sw + (BC + RPG * NW * i + RPG * wave) * ROWB + lane * 16);
+        v[i] = lds_read16(pa[i]);
+        v[GB + i] = lds_read16(pa[i] + BP * ROWB);
+      }
+      lds_wait_all<2 * GB + 6>(v);
+      float cA[8], cB[8], cD[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        cA[e] = __uint_as_float(v[2 * GB + (e >> 2)][e & 3]);
+        cB[e] = __uint_as_float(v[2 * GB + 2 + (e >> 2)][e & 3]);
+        cD[e] = __uint_as_float(v[2 * GB + 4 + (e >> 2)][e & 3]);
+      }
+#pragma unroll
+      for (int i = 0; i < GB; ++i) {
+        float g8[8], x8[8];
+        unpack8v(v[i], g8);
+        unpack8v(v[GB + i], x8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g8[e] = fmaf(cA[e], g8[e], fmaf(cB[e], x8[e], cD[e]));
+        u32x4_t o = pack8v(g8);
+        const unsigned msk = ((ok >> i) & 1u) ? 0xffffffffu : 0u;  // padding / rows past M stay zero
+        o.x &= msk;
+        o.y &= msk;
+        o.z &= msk;
+        o.w &= msk;
+        lds_write16(pa[i], o);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if ((xci += BK) == C) {
+        xci = 0;
+        if (++xs == a.S) {
+          xs = 0;
+          ++xr;
+        }
+      }
+    }
     if constexpr (PRO) {
       char* sw = smem + (t % NS) * STAGE;
       // one LDS round trip: this stage's scale/shift and the lane's landed pieces together
@@ -826,15 +915,15 @@ static int cfin_max_blocks() {
   return v;
 }
 
-template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF, int BK, bool PRO, bool SROW = false>
+template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF, int BK, bool PRO, bool SROW = false, bool BNB = false>
 static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
   const int T = a->C == 8 || a->C == 16 ? a->R : (a->R * a->S * a->C) / BK;  // k-stages (SROW: filter rows)
-  const int LDS0 = (T < NS ? T : NS) * (BC + BP) * BK * 2;         // stage slots actually used
-  const int lds_main = LDS0 + (PRO ? 8 * a->C : 0);                 // + fused-BN scale/shift
+  const int LDS0 = (T < NS ? T : NS) * (BC + BP * (BNB ? 2 : 1)) * BK * 2;  // stage slots actually used
+  const int lds_main = LDS0 + (PRO ? 8 * a->C : 0) + (BNB ? 12 * a->C : 0);  // + fused-BN parameters
   const int LDS = lds_main > BP * BC * 4 ? lds_main : BP * BC * 4;  // epilogue staging tile
   if (LDS > 160 * 1024) return (int)hipErrorInvalidValue;
   static bool attr_set = false;
-  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS, NW, PF, BK, PRO, SROW>;
+  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS, NW, PF, BK, PRO, SROW, BNB>;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
@@ -875,6 +964,12 @@ static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t str
     return (int)hipErrorInvalidValue;
   }
   if (a->C % BK) return (int)hipErrorInvalidValue;
+  if (a->bnb_x != nullptr) {  // fused BN-backward input (data gradients): 64-deep stages only
+    if constexpr (BK == 64)
+      return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, false, false, true>(a, zero, stream)
+                : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false, false, true>(a, zero, stream);
+    return (int)hipErrorInvalidValue;
+  }
   if (a->in_scale != nullptr)
     return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, true>(a, zero, stream)
               : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, true>(a, zero, stream);
@@ -992,6 +1087,8 @@ DRN_API int drn_conv_mt_ok(const DrnConvFwdArgs* a);
 
 // Whether the LDS-DMA kernel family supports this convolution.
 DRN_API int drn_conv_glds_ok(const DrnConvFwdArgs* a) {
+  if (a->bnb_x != nullptr)  // fused BN-backward input: LDS-DMA 64-deep stages only
+    return a->C % 64 == 0 && a->C <= 4096 && a->dil == 1 && a->in_scale == nullptr;
   if (a->C == 8 || a->C == 16)  // row-staged narrow conv (stem, CIFAR stage 1)
     return a->dil == 1 && a->S * a->C <= 64 && (a->in_scale == nullptr || a->relu_in != 0);
   return a->C % 32 == 0 && a->dil == 1 && (a->in_scale == nullptr || (a->C <= 4096 && a->relu_in != 0));
@@ -1007,6 +1104,8 @@ DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
       (a->in_scale == nullptr || a->in_fin.C != a->C || a->in_fin.G < 1 || a->in_fin.G > DRN_BN_FIN_GMAX))
     return (int)hipErrorInvalidValue;
   if (a->cfg >= DRN_GLDS_NCFG && a->cfg != 100) return drn_conv_mt(a->cfg - DRN_GLDS_NCFG, a, zero, s);
+  if (a->bnb_x != nullptr && (!drn_conv_glds_ok(a) || zero == nullptr || a->cfg == 100))
+    return (int)hipErrorInvalidValue;  // the BN-backward input transform exists on the LDS-DMA path only
   if (drn_conv_glds_ok(a) && zero != nullptr && a->cfg != 100)
     return drn::launch_glds_cfg(a->cfg >= 0 ? a->cfg : drn::glds_default_cfg(a), a, zero, s);
   if (a->in_fin.stats != nullptr) {
@@ -1024,6 +1123,10 @@ DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
 // diagnostics: per-workgroup timeline buffer for the LDS-DMA conv kernel (nullptr disables)
 DRN_API int drn_conv_trace_set(unsigned long long* buf) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(drn::g_conv_trace), &buf, sizeof(buf));
+}
+
+DRN_API int drn_conv_set_flags(int flags) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(drn::g_conv_flags), &flags, sizeof(flags));
 }
 
 DRN_API int drn_conv_glds_cfg_bp(int cfg) { return drn::glds_cfg_bp(cfg); }

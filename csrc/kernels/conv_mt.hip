@@ -514,7 +514,7 @@ DRN_API int drn_conv_mt_num_cfgs() { return 9; }
 DRN_API int drn_conv_mt_ok(const DrnConvFwdArgs* a) {
   return a->C % 64 == 0 && a->K % 8 == 0 && a->dil == 1 && a->fin_cnt == nullptr && a->out_fill == 0 &&
          (a->in_scale == nullptr || (a->C <= 4096 && a->relu_in != 0)) &&
-         !(a->in_scale != nullptr && a->bn_x != nullptr);
+         !(a->in_scale != nullptr && a->bn_x != nullptr) && a->bnb_x == nullptr;
 }
 
 DRN_API int drn_conv_mt(int cfg, DrnConvFwdArgs* a, const void* zero, hipStream_t s) {

@@ -312,17 +312,23 @@ __device__ __forceinline__ void lgkm_fence(s16x4v (&a)[MI][2], s16x4v (&b)[MJ][2
 // counted vmcnt wait each lane rewrites the pieces its own LDS-DMAs landed for the stage (the
 // lane's channels are fixed for the whole kernel, so scale/shift stay in registers) and the
 // stage's barrier publishes them. Zero-page pieces (padding, pixels past the split) stay zero.
-template <int BKK, int BCO, int NS, int BP = 64, bool PRO = false>
+//
+// BNB: dY is dx of a BatchNorm whose apply was not materialised (DrnConvWgradArgs::bnb_x):
+// each stage also DMAs the BatchNorm-input pieces (an X image behind the dY image) and every
+// lane rewrites its own landed dY pieces as A*g + B*x + D (its 8 channels are fixed for the
+// kernel, so the coefficients live in registers; they are finalized once per workgroup from the
+// backward statistics); pieces past the split / the channel range stay zero.
+template <int BKK, int BCO, int NS, int BP = 64, bool PRO = false, bool BNB = false>
 __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a, const void* __restrict__ zero) {
   static_assert(BP == 32 || BP == 64, "pixels per stage");
   constexpr int KS = BP / 32;  // 32-deep MFMA k-slices per stage
   constexpr int WA = BKK * 2, WB = BCO * 2;       // image row bytes
   constexpr int A_BYTES = BP * WA;
-  constexpr int STAGE = A_BYTES + BP * WB;
+  constexpr int STAGE = A_BYTES + BP * WB * (BNB ? 2 : 1);
   constexpr int LPA = WA / 16, LPB = WB / 16;     // lanes per row in one wave-instruction
   constexpr int RIA = 64 / LPA, RIB = 64 / LPB;   // rows per wave-instruction
   constexpr int IA = BP / RIA / 4, IB = BP / RIB / 4;  // instructions per wave per stage
-  constexpr int G = IA + IB;
+  constexpr int G = IA + IB * (BNB ? 2 : 1);
   constexpr int D = NS - 1;
   constexpr int WKK = BKK / 2, WCO = BCO / 2;
   constexpr int MI = WKK / 16, MJ = WCO / 16;
@@ -386,6 +392,30 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
   const bool cvalid = dc < a.K;
   const bf16_t* __restrict__ xg = reinterpret_cast<const bf16_t*>(a.x);
   const bf16_t* __restrict__ dyg = reinterpret_cast<const bf16_t*>(a.dy) + dc;
+  const bf16_t* __restrict__ bxg = BNB ? reinterpret_cast<const bf16_t*>(a.bnb_x) + dc : nullptr;
+  float bA[8], bB[8], bD[8];  // BNB: this lane's 8 dY channels' coefficients
+  if constexpr (BNB) {
+    // finalize the block's BCO channels into LDS (behind the pipeline stages), then each lane
+    // takes its 8; retired before any LDS-DMA is in flight
+    float* cf = reinterpret_cast<float*>(smem + NS * STAGE);
+    for (int cl = threadIdx.x; cl < BCO; cl += 256) {
+      const int c = c0 + cl;
+      float A = 0.f, B = 0.f, D = 0.f;
+      if (c < a.K) drn_bn_fin_bwd(a.bnb_fin, c, false, A, B, D);
+      cf[cl] = A;
+      cf[BCO + cl] = B;
+      cf[2 * BCO + cl] = D;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bA[e] = cf[blc * 8 + e];
+      bB[e] = cf[BCO + blc * 8 + e];
+      bD[e] = cf[2 * BCO + blc * 8 + e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) asm volatile("" : "+v"(bA[e]), "+v"(bB[e]), "+v"(bD[e]));
+  }
   // Pixel coordinates of this lane's A rows, decoded once and then advanced by 64 pixels per
   // stage with adds/compares (a magic-number division per row per stage made the loader
   // VALU-bound: mul_hi/mul_lo/64-bit mads are quarter rate). Offsets use 24-bit multiplies
@@ -439,6 +469,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
       const void* src = (cvalid && m < mend) ? (const void*)(dyg + (uint32_t)__mul24(m, a.K)) : zero;
       __builtin_amdgcn_global_load_lds((wg_gbl_void*)src, (wg_lds_void*)(st + A_BYTES + r0 * WB), 16, 0, 0);
     }
+    if constexpr (BNB) {
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        const int r0 = RIB * (wave + 4 * i);
+        const int m = mstep + r0 + brow;
+        const void* src = (cvalid && m < mend) ? (const void*)(bxg + (uint32_t)__mul24(m, a.K)) : zero;
+        __builtin_amdgcn_global_load_lds((wg_gbl_void*)src, (wg_lds_void*)(st + A_BYTES + BP * WB + r0 * WB), 16,
+                                         0, 0);
+      }
+    }
   };
 
   f32x4_t acc[MI][MJ];
@@ -479,6 +519,37 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
       }
       lds_wait_all<IA>(v);
       lds_bn_relu_store<IA, true>(pa, v, (okm >> (slot * IA)) & ((1u << IA) - 1u), psc2, psh2);
+    }
+    if constexpr (BNB) {
+      const int slot = t % NS;
+      char* sw = smem + slot * STAGE + A_BYTES;
+      const int mstep = mbeg + t * BP;
+      uint32_t pb[IB];
+      u32x4_t v[2 * IB];
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        pb[i] = lds_addr(sw + RIB * (wave + 4 * i) * WB + lane * 16);
+        v[i] = lds_read16(pb[i]);
+        v[IB + i] = lds_read16(pb[i] + BP * WB);
+      }
+      lds_wait_all<2 * IB>(v);
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        float g8[8], x8[8];
+        unpack8v(v[i], g8);
+        unpack8v(v[IB + i], x8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) g8[e] = fmaf(bA[e], g8[e], fmaf(bB[e], x8[e], bD[e]));
+        u32x4_t o = pack8v(g8);
+        const bool ok = cvalid && mstep + RIB * (wave + 4 * i) + brow < mend;
+        const unsigned msk = ok ? 0xffffffffu : 0u;
+        o.x &= msk;
+        o.y &= msk;
+        o.z &= msk;
+        o.w &= msk;
+        lds_write16(pb[i], o);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -536,11 +607,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
     }
 }
 
-template <int BKK, int BCO, int NS, int BP, bool PRO>
+template <int BKK, int BCO, int NS, int BP, bool PRO, bool BNB = false>
 static int launch_wgrad_glds_p(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
-  constexpr int LDS = NS * (BP * BKK * 2 + BP * BCO * 2);
+  constexpr int LDS = NS * (BP * BKK * 2 + BP * BCO * 2 * (BNB ? 2 : 1)) + (BNB ? 12 * BCO : 0);
   static bool attr_set = false;
-  auto kern = conv_wgrad_glds_kernel<BKK, BCO, NS, BP, PRO>;
+  auto kern = conv_wgrad_glds_kernel<BKK, BCO, NS, BP, PRO, BNB>;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
@@ -554,6 +625,10 @@ static int launch_wgrad_glds_p(DrnConvWgradArgs* a, const void* zero, hipStream_
 
 template <int BKK, int BCO, int NS, int BP = 64>
 static int launch_wgrad_glds(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
+  if (a->bnb_x != nullptr) {
+    if (a->in_scale != nullptr) return launch_wgrad_glds_p<BKK, BCO, NS, BP, true, true>(a, zero, s);
+    return launch_wgrad_glds_p<BKK, BCO, NS, BP, false, true>(a, zero, s);
+  }
   if (a->in_scale != nullptr) return launch_wgrad_glds_p<BKK, BCO, NS, BP, true>(a, zero, s);
   return launch_wgrad_glds_p<BKK, BCO, NS, BP, false>(a, zero, s);
 }
@@ -651,6 +726,7 @@ DRN_API int drn_wgrad_tiles(int Ktot, int K) {
 DRN_API int drn_conv_wgrad(DrnConvWgradArgs* a, hipStream_t s) {
   if ((a->C % 8) != 0 || (a->K % 8) != 0 || a->splits < 1 || (a->pix_per_split % 64) != 0)
     return (int)hipErrorInvalidValue;
+  if (a->bnb_x != nullptr) return (int)hipErrorInvalidValue;  // BN-backward dY: LDS-DMA kernels only
   return a->in_scale != nullptr ? drn::dispatch_wgrad<true>(a, s) : drn::dispatch_wgrad<false>(a, s);
 }
 
@@ -659,6 +735,8 @@ DRN_API int drn_conv_wgrad2(DrnConvWgradArgs* a, const void* zero, int ns, hipSt
   if ((a->C % 8) != 0 || (a->K % 8) != 0 || a->splits < 1 || (a->pix_per_split % 64) != 0)
     return (int)hipErrorInvalidValue;
   // the LDS-DMA kernels' fused BN prologue always applies the ReLU (pre-activation v2)
+  if (a->bnb_x != nullptr && (zero == nullptr || ns == 0 || (a->in_scale != nullptr && a->relu_in == 0)))
+    return (int)hipErrorInvalidValue;
   if (zero == nullptr || ns == 0 || (a->in_scale != nullptr && a->relu_in == 0)) return drn_conv_wgrad(a, s);
   return drn::dispatch_wgrad_glds(a, zero, ns, s);
 }

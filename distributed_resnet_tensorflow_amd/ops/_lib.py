@@ -16,7 +16,9 @@ import torch  # noqa: F401  (must be imported first: its HIP runtime is the one 
 
 _LIB = None
 _LOCK = threading.Lock()
-LIB_PATH = Path(__file__).resolve().parent / "libdrn_kernels.so"
+LIB_PATH = Path(os.environ.get("DRN_KERNEL_LIB") or Path(__file__).resolve().parent / "libdrn_kernels.so")
+# diagnostics-only entry points an older library (A/B runs via DRN_KERNEL_LIB) may lack
+_OPTIONAL = {"drn_conv_trace_set", "drn_conv_set_flags"}
 
 c_int = ctypes.c_int
 c_i64 = ctypes.c_int64
@@ -61,6 +63,7 @@ class DrnConvFwdArgs(ctypes.Structure):
         ("fin_scale", c_p), ("fin_shift", c_p), ("fin_mean", c_p), ("fin_invstd", c_p),
         ("fin_dgamma", c_p), ("fin_dbeta", c_p), ("fin_coef", c_p),
         ("fd_pq", DrnFastDiv), ("fd_q", DrnFastDiv), ("in_fin", DrnBnFin),
+        ("bnb_x", c_p), ("bnb_fin", DrnBnFin),
     ]
 
 
@@ -70,6 +73,7 @@ class DrnConvWgradArgs(ctypes.Structure):
         ("N", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("K", c_int), ("R", c_int), ("S", c_int),
         ("P", c_int), ("Q", c_int), ("stride", c_int), ("pad_h", c_int), ("pad_w", c_int), ("relu_in", c_int),
         ("splits", c_int), ("pix_per_split", c_int), ("fd_pq", DrnFastDiv), ("fd_q", DrnFastDiv),
+        ("bnb_x", c_p), ("bnb_fin", DrnBnFin),
     ]
 
 
@@ -81,6 +85,7 @@ _SIGS = {
     "drn_conv_glds_ok": ([ctypes.POINTER(DrnConvFwdArgs)], c_int),
     "drn_conv_glds_num_cfgs": ([], c_int),
     "drn_conv_trace_set": ([c_p], c_int),
+    "drn_conv_set_flags": ([c_int], c_int),
     "drn_conv_glds_default_cfg": ([ctypes.POINTER(DrnConvFwdArgs)], c_int),
     "drn_conv_wgrad": ([ctypes.POINTER(DrnConvWgradArgs), c_p], c_int),
     "drn_conv_wgrad2": ([ctypes.POINTER(DrnConvWgradArgs), c_p, c_int, c_p], c_int),
@@ -118,6 +123,7 @@ _SIGS = {
     "drn_p2p_args_size": ([], c_int),
     "drn_bn_fin_size": ([], c_int),
     "drn_conv_args_size": ([], c_int),
+    "drn_wgrad_args_size": ([], c_int),
     "drn_bn_fin_fwd_launch": ([c_p, c_p], c_int),
     "drn_bn_apply_fin": ([c_p, c_p, c_p, c_i64, c_int, c_int, c_p], c_int),
     "drn_bn_bwd_apply_fin": ([c_p, c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_p], c_int),
@@ -153,10 +159,13 @@ def lib():
         except OSError as e:  # pragma: no cover
             raise KernelLibraryError(f"failed to load {LIB_PATH}: {e}") from e
         for name, (args, res) in _SIGS.items():
+            if name in _OPTIONAL and not hasattr(h, name):
+                continue
             fn = getattr(h, name)
             fn.argtypes = args
             fn.restype = res
-        for name, st in (("drn_bn_fin_size", DrnBnFin), ("drn_conv_args_size", DrnConvFwdArgs)):
+        for name, st in (("drn_bn_fin_size", DrnBnFin), ("drn_conv_args_size", DrnConvFwdArgs),
+                         ("drn_wgrad_args_size", DrnConvWgradArgs)):
             if getattr(h, name)() != ctypes.sizeof(st):
                 raise KernelLibraryError(f"{st.__name__} layout mismatch between Python and {LIB_PATH.name}")
         _LIB = h

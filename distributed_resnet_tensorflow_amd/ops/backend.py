@@ -234,13 +234,16 @@ class HipBackend(_Common):
         forced = os.environ.get("DRN_WGRAD_NS")
         self.forced_wgrad_ns = int(forced) if forced not in (None, "") else None
         self.tune_log: list = []
+        flags = os.environ.get("DRN_CONV_FLAGS")  # conv cache-policy switches (conv_fwd.hip g_conv_flags)
+        if flags not in (None, ""):
+            _lib.check(self.L.drn_conv_set_flags(int(flags)), "drn_conv_set_flags")
 
     def stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream
 
     # -- conv ---------------------------------------------------------------------------------
     def conv_args(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None,
-                  bn_bwd=None, bn_fin: Optional[BnFin] = None, in_fin: Optional[BnCfin] = None):
+                  bn_bwd=None, bn_fin: Optional[BnFin] = None, in_fin: Optional[BnCfin] = None, bnb=None):
         N, H, W, C = x.shape
         K, R, S, C2 = w.shape
         N2, P, Q, K2 = y.shape
@@ -289,6 +292,11 @@ class HipBackend(_Common):
             assert in_bn is not None and in_fin.C == C, "the consumer-side finalize feeds the fused BN prologue"
             _aligned16(in_fin.stats)
             a.in_fin = in_fin.struct()
+        if bnb is not None:  # (bn_input, BnCfin): x is the masked BN-backward gradient g
+            bx, bf = bnb
+            assert bx.shape == x.shape and in_bn is None and bf.C == C
+            a.bnb_x = bx.data_ptr()
+            a.bnb_fin = bf.struct()
         a.cfg = self.forced_cfg if self.forced_cfg is not None else self.conv_cfg.get(self.conv_key(a), -1)
         return a
 
@@ -296,7 +304,7 @@ class HipBackend(_Common):
     def conv_key(a) -> tuple:
         return (a.N, a.H, a.W, a.C, a.K, a.R, a.S, a.P, a.Q, a.stride, a.pad_h, a.pad_w, a.dil,
                 a.in_scale is not None, a.out_stride, a.residual is not None, a.bn_x is not None,
-                a.stats is not None)
+                a.stats is not None, a.bnb_x is not None)
 
     def launch_conv(self, a):
         if a.cfg == -1 and self.autotune and self.forced_cfg is None:
@@ -322,41 +330,54 @@ class HipBackend(_Common):
         ctypes.memmove(ctypes.addressof(t), ctypes.addressof(a), ctypes.sizeof(a))
         t.y = y.data_ptr()
         if a.residual is not None and a.residual == a.y:
-            t.residual = None
+            t.residual = t.y  # accumulating launch: time the same in-place epilogue on the scratch output
         if a.stats is not None:
             t.stats = st.data_ptr()
         t.fin_cnt = None  # timing runs must not finalize (moving averages) the live BN
         t.in_fin.publish = 0
-        best, best_t = 100, float("inf")
+        t.bnb_fin.publish = 0
         s = self.stream()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         cands = os.environ.get("DRN_CONV_CANDS")
         cands = [int(c) for c in cands.split(",")] if cands else [100] + list(range(self.L.drn_conv_glds_num_cfgs()))
+
+        def time_cfg(cfg, n):
+            t.cfg = cfg
+            _lib.check(self.L.drn_conv_fwd2(ctypes.byref(t), self.zero_page.data_ptr(), s), "drn_conv_fwd")
+            ev0.record()
+            for _ in range(n):
+                _lib.check(self.L.drn_conv_fwd2(ctypes.byref(t), self.zero_page.data_ptr(), s), "drn_conv_fwd")
+            ev1.record()
+            ev1.synchronize()
+            return ev0.elapsed_time(ev1) / n
+
+        # pass 1: every applicable configuration, short; pass 2: the 4 fastest re-timed twice,
+        # interleaved, keeping each one's best (single short timings picked outliers: clock
+        # ramps and neighbours' cache state moved the choice by >10 %)
+        first = []
         for cfg in cands:
             t.cfg = cfg
             if self.L.drn_conv_fwd2(ctypes.byref(t), self.zero_page.data_ptr(), s) != 0:
                 continue  # configuration not applicable to this geometry (e.g. C % 64 != 0)
-            for _ in range(1):
-                _lib.check(self.L.drn_conv_fwd2(ctypes.byref(t), self.zero_page.data_ptr(), s), "drn_conv_fwd")
-            ev0.record()
-            for _ in range(iters):
-                _lib.check(self.L.drn_conv_fwd2(ctypes.byref(t), self.zero_page.data_ptr(), s), "drn_conv_fwd")
-            ev1.record()
-            ev1.synchronize()
-            ms = ev0.elapsed_time(ev1) / iters
-            if ms < best_t:
-                best, best_t = cfg, ms
+            first.append((time_cfg(cfg, iters), cfg))
+        first.sort()
+        top = {cfg: ms for ms, cfg in first[:4 if os.environ.get("DRN_TUNE_2PASS", "1") == "1" else 1]}
+        for _ in range(2 if len(top) > 1 else 0):
+            for cfg in list(top):
+                top[cfg] = min(top[cfg], time_cfg(cfg, 2 * iters))
+        best, best_t = min(top.items(), key=lambda kv: kv[1]) if top else (100, 0.0)
         self.tune_log.append((key, best, round(best_t * 1e3, 1)))
         return best
 
     def conv_fwd(self, x, w, y, g, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None, bn_bwd=None,
-                 bn_fin: Optional[BnFin] = None, out_fill: bool = False, in_fin: Optional[BnCfin] = None):
+                 bn_fin: Optional[BnFin] = None, out_fill: bool = False, in_fin: Optional[BnCfin] = None,
+                 bnb=None):
         """y = conv(x) (+ residual); optional BN statistics of y, or (bn_bwd = (x_bn, scale, shift,
         mean, invstd)) the fused BN-backward reduction with ReLU-masked output; bn_fin finalizes
         that BN in the same launch. out_fill (strided out_map, single-phase output): the epilogue
         also writes zeros at every other phase position, so y needs no separate clearing.
         in_fin: the input BN (in_bn) is finalized by this conv's prologue (BnCfin)."""
-        a = self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd, bn_fin, in_fin)
+        a = self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd, bn_fin, in_fin, bnb)
         if out_fill:
             assert out_map is not None and bn_bwd is None and residual is None, "out_fill: plain strided output only"
             a.out_fill = 1
@@ -385,7 +406,8 @@ class HipBackend(_Common):
     # traffic of the default 512-block target is ~1.7 GB per ResNet-50 step
     WGRAD_TARGETS = tuple(int(v) for v in os.environ.get("DRN_WGRAD_TARGETS", "128,256,512").split(","))
 
-    def wgrad_args(self, x, dy, out, g: ConvGeom, in_bn=None, relu_in=True, ws=None, target_blocks: int = 0):
+    def wgrad_args(self, x, dy, out, g: ConvGeom, in_bn=None, relu_in=True, ws=None, target_blocks: int = 0,
+                   bnb=None):
         N, H, W, C = x.shape
         N2, P, Q, K = dy.shape
         Kd, R, S, Cd = out.shape
@@ -402,6 +424,13 @@ class HipBackend(_Common):
         a.splits, a.pix_per_split = splits, pps
         a.fd_pq = _lib.DrnFastDiv.make(P * Q)
         a.fd_q = _lib.DrnFastDiv.make(Q)
+        if bnb is not None:  # dY is the masked BN-backward gradient g; dY_eff = A*g + B*bn_input + D
+            bx, bf = bnb
+            assert bx.shape == dy.shape and bf.C == K
+            a.bnb_x = bx.data_ptr()
+            f = bf.struct()
+            f.publish = 0  # the data-gradient consumer publishes dgamma / dbeta
+            a.bnb_fin = f
         if splits == 1:
             a.out = out.data_ptr()
         else:
@@ -421,7 +450,8 @@ class HipBackend(_Common):
 
     @staticmethod
     def wgrad_key(a) -> tuple:
-        return (a.N, a.H, a.W, a.C, a.K, a.R, a.S, a.P, a.Q, a.stride, a.pad_h, a.pad_w, a.in_scale is not None)
+        return (a.N, a.H, a.W, a.C, a.K, a.R, a.S, a.P, a.Q, a.stride, a.pad_h, a.pad_w, a.in_scale is not None,
+                a.bnb_x is not None)
 
     def _wgrad_kernel(self, a, ns: int, st):
         _lib.check(self.L.drn_conv_wgrad2(ctypes.byref(a), self.zero_page.data_ptr(), ns, st), "drn_conv_wgrad")
@@ -448,6 +478,8 @@ class HipBackend(_Common):
                 continue
             seen.add(a.splits)
             for ns in cands:
+                if self.L.drn_conv_wgrad2(ctypes.byref(a), self.zero_page.data_ptr(), ns, st) != 0:
+                    continue  # pipeline not available for this launch (e.g. BN-backward dY: LDS-DMA only)
                 for _ in range(2):
                     self._wgrad_full(a, ns, out, st)
                 ev0.record()
@@ -461,8 +493,8 @@ class HipBackend(_Common):
         self.tune_log.append((("wgrad",) + key, best, round(best_t * 1e3, 1)))
         return best
 
-    def conv_wgrad(self, x, dy, out, g, in_bn=None, relu_in=True, ws=None):
-        args_for = lambda tgt: self.wgrad_args(x, dy, out, g, in_bn, relu_in, ws, tgt)
+    def conv_wgrad(self, x, dy, out, g, in_bn=None, relu_in=True, ws=None, bnb=None):
+        args_for = lambda tgt: self.wgrad_args(x, dy, out, g, in_bn, relu_in, ws, tgt, bnb)
         a = args_for(0)
         st = self.stream()
         if self.forced_wgrad_ns is not None:
@@ -472,6 +504,8 @@ class HipBackend(_Common):
         if key not in self.wgrad_ns and self.autotune and not torch.cuda.is_current_stream_capturing():
             self.wgrad_ns[key] = self._tune_wgrad(args_for, out, key)
         tgt, ns = self.wgrad_ns.get(key, (0, 2))
+        if ns == 0 and a.bnb_x is not None:
+            ns = 2
         if tgt:
             a = args_for(tgt)
         self._wgrad_full(a, ns, out, st)
@@ -711,9 +745,12 @@ class RefBackend(_Common):
         return None
 
     def conv_fwd(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None,
-                 bn_bwd=None, bn_fin: Optional[BnFin] = None, out_fill: bool = False, in_fin: Optional[BnCfin] = None):
+                 bn_bwd=None, bn_fin: Optional[BnFin] = None, out_fill: bool = False, in_fin: Optional[BnCfin] = None,
+                 bnb=None):
         if in_fin is not None and in_fin.publish:
             self._publish_fwd(in_fin)
+        if bnb is not None:
+            x = self._bnb(x, bnb)
         self._conv_fwd(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd, out_fill)
         if bn_fin is not None:
             f, G = bn_fin, stats.numel() // (2 * w.shape[0])
@@ -761,7 +798,25 @@ class RefBackend(_Common):
     def wgrad_ws_elems(self, M, K, R, S, C):
         return 0
 
-    def conv_wgrad(self, x, dy, out, g: ConvGeom, in_bn=None, relu_in=True, ws=None):
+    def _bnb(self, gr, bnb, publish: bool = True):
+        """dY of a non-materialised BatchNorm backward (the HIP kernels' BNB prologue):
+        dx = gamma*invstd * (g - mean(g) - xhat * mean(g*xhat)) from the backward statistics
+        replicas, which stay intact for the other consumer; the publishing consumer writes
+        dgamma / dbeta."""
+        bx, f = bnb
+        C = f.C
+        p = f.stats.view(f.G, 2, C).double().sum(0)
+        k1 = (f.gamma * f.invstd).double()
+        xh = (bx.double() - f.mean.double()) * f.invstd.double()
+        dx = k1 * (gr.double() - p[0] / f.count - xh * (p[1] / f.count))
+        if publish and f.publish:
+            f.dbeta.copy_(p[0].to(f.dbeta.dtype))
+            f.dgamma.copy_(p[1].to(f.dgamma.dtype))
+        return dx.to(gr.dtype)
+
+    def conv_wgrad(self, x, dy, out, g: ConvGeom, in_bn=None, relu_in=True, ws=None, bnb=None):
+        if bnb is not None:
+            dy = self._bnb(dy, bnb, publish=False)
         K, R, S, C = out.shape
         _, P, Q, _ = dy.shape
         xc = _pad_for(_pre(x, in_bn, relu_in).permute(0, 3, 1, 2), P, Q, R, S, g)

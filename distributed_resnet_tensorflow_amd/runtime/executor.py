@@ -110,6 +110,13 @@ class Executor:
         self.spec, self.N, self.be = spec, batch, backend
         # fuse each BN's backward reduction into the epilogue of the data-gradient conv feeding it
         self.fuse_bn_bwd = os.environ.get("DRN_FUSE_BN_BWD", "1") == "1"
+        # BN backward of the 3x3 conv's input fused into the 1x1 conv's weight / data gradients
+        # (BNB prologue: no materialised apply). Tested, but OFF by default: the 1x1 data
+        # gradient re-reads its narrow input once per output-channel tile (4-8x), so the extra
+        # BN-input DMA and the in-LDS transform cost more than the apply pass they replace
+        # (ResNet-50 bs128, scripts/op_breakdown.py: applies -330 us, consumers +800 us; step
+        # 10.74 -> 11.18 ms)
+        self.fuse_bnb = os.environ.get("DRN_FUSE_BNB", "0") == "1"
         # debug mode: synchronous finiteness checks after every block (forward and backward)
         self.check_nan = os.environ.get("DRN_CHECK_NAN", "0") == "1"
         # deterministic mode (DRN_DETERMINISTIC=1): bitwise-reproducible steps -- one statistics
@@ -657,14 +664,14 @@ class Executor:
             self.grad_ready(lo)
 
     # -- weight gradients on the side stream ---------------------------------------------------------
-    def _wgrad(self, x, dy, dw, geom, in_bn=None, dy_buf=None):
+    def _wgrad(self, x, dy, dw, geom, in_bn=None, dy_buf=None, bnb=None):
         if self.side is None:
-            self.be.conv_wgrad(x, dy, dw, geom, in_bn=in_bn, ws=self.wgrad_ws)
+            self.be.conv_wgrad(x, dy, dw, geom, in_bn=in_bn, ws=self.wgrad_ws, bnb=bnb)
             return
         main = torch.cuda.current_stream(self.device)
         self.side.wait_stream(main)                      # x and dy are complete
         with torch.cuda.stream(self.side):
-            self.be.conv_wgrad(x, dy, dw, geom, in_bn=in_bn, ws=self.wgrad_ws)
+            self.be.conv_wgrad(x, dy, dw, geom, in_bn=in_bn, ws=self.wgrad_ws, bnb=bnb)
         if dy_buf is not None:                           # the main stream must not overwrite dy early
             ev = torch.cuda.Event()
             ev.record(self.side)
@@ -687,7 +694,7 @@ class Executor:
         else:
             main.wait_event(ev)
 
-    def _dgrad(self, op: ConvOp, dy, dx, accumulate: bool, bn: Optional[BNState] = None, bn_x=None):
+    def _dgrad(self, op: ConvOp, dy, dx, accumulate: bool, bn: Optional[BNState] = None, bn_x=None, bnb=None):
         """Data gradient of `op` into dx (+= when accumulate). With bn set (requires a launch set
         covering every dx element) the epilogue also performs that BN's backward reduction."""
         # a single-phase strided data gradient (1x1 stride-2 projection) writes the zeros of the
@@ -708,7 +715,7 @@ class Executor:
         for k, ph in enumerate(op.dg):
             self.be.conv_fwd(dy, ph.wt, dx, ph.geom, residual=dx if accumulate else None, out_map=ph.out_map,
                              stats=bn.bacc if fuse is not None else None, bn_bwd=fuse,
-                             bn_fin=fin if k == last else None, out_fill=fill)
+                             bn_fin=fin if k == last else None, out_fill=fill, bnb=bnb)
 
     def _block_bwd(self, bp: BlockPlan, bufs, cur: int) -> int:
         """Back-propagates one block; bufs[cur] holds d(block output). Returns the index of the
@@ -720,12 +727,13 @@ class Executor:
         d_out = self._view(bufs[cur], bp.out)
         ins = [bp.x] + bp.hs                 # raw inputs of each main-path conv
         dy, dy_buf, dy_k = d_out, bufs[cur], cur
+        lazy = None  # (bn input, BnCfin): dy is the masked gradient g of a non-materialised BN backward
         for i in reversed(range(len(bp.convs))):
             op, xin, b = bp.convs[i], ins[i], bp.bn[i]
             tgt_k = self._take(bufs, (cur, dy_k))
             tgt = bufs[tgt_k]
             a_in, pro = (b.act, None) if b.act is not None else (b.src, b.ss)
-            self._wgrad(a_in, dy, op.dw, op.geom, in_bn=pro, dy_buf=dy_buf)
+            self._wgrad(a_in, dy, op.dw, op.geom, in_bn=pro, dy_buf=dy_buf, bnb=lazy)
             self._claim(tgt)
             da = self._view(tgt, xin)        # d relu(bn(xin))
             add = None
@@ -736,14 +744,32 @@ class Executor:
                 pj = bp.proj
                 self._wgrad(a_in, d_out, pj.dw, pj.geom, in_bn=pro, dy_buf=bufs[cur])
                 self._dgrad(pj, d_out, da, accumulate=False)
-                self._dgrad(op, dy, da, accumulate=True, bn=b if fuse else None, bn_x=xin)
+                self._dgrad(op, dy, da, accumulate=True, bn=b if fuse else None, bn_x=xin, bnb=lazy)
             else:
-                self._dgrad(op, dy, da, accumulate=False, bn=b if fuse else None, bn_x=xin)
+                self._dgrad(op, dy, da, accumulate=False, bn=b if fuse else None, bn_x=xin, bnb=lazy)
                 if i == 0:
                     add = d_out              # identity shortcut
-            self._bn_bwd(b, xin, da, da, add=add, reduced=fuse)
+            lazy = None
+            if fuse and self._bnb_ok(bp, i, xin):
+                # the BN backward of conv i's input is not materialised: both consumers (the
+                # previous conv's weight and data gradients, 1x1) apply it to g on load
+                lazy = (xin, BnCfin(b.bacc, float(xin.numel() // b.bn.c), b.gamma, mean=b.mean, invstd=b.invstd,
+                                    dgamma=b.dgamma, dbeta=b.dbeta, publish=True))
+            else:
+                self._bn_bwd(b, xin, da, da, add=add, reduced=fuse)
             dy, dy_buf, dy_k = da, tgt, tgt_k
         return dy_k
+
+    def _bnb_ok(self, bp: BlockPlan, i: int, xin) -> bool:
+        """Whether the BN backward feeding conv i-1 can be fused into that conv's consumers:
+        interior BN (i >= 1, no residual add), consumer a 1x1 stride-1 conv whose data gradient is
+        one full-cover launch, channels on the LDS-DMA path (C % 64 == 0), consumer-side
+        finalize mode (DRN_FUSE_BNB=0 keeps the materialised apply)."""
+        if not self.fuse_bnb or i < 1 or not self.cfin:
+            return False
+        prev = bp.convs[i - 1]
+        return prev.conv.k == 1 and prev.conv.stride == 1 and prev.full_cover and len(prev.dg) == 1 \
+            and xin.shape[-1] % 64 == 0
 
     def _take(self, bufs, busy) -> int:
         """Index of the least recently used gradient buffer not holding a live gradient (`busy`);
