@@ -26,16 +26,17 @@
 
 namespace drn {
 
-// Optional per-workgroup timeline of the LDS-DMA conv kernel (diagnostics only; null in normal
-// runs): record b = {start, main-loop end, end} in s_memrealtime ticks (100 MHz) + HW_ID / XCC_ID.
+// Optional per-workgroup timeline of the LDS-DMA conv kernel, compiled in only with
+// -DDRN_CONV_TRACE (even a never-taken check costs ~2.5 % of the ResNet-50 step): record
+// b = {start, main-loop end, end} in s_memrealtime ticks (100 MHz) + HW_ID / XCC_ID.
+#ifdef DRN_CONV_TRACE
 __device__ unsigned long long* g_conv_trace = nullptr;
+#endif
 
-// Cache-policy switch of the conv epilogue (drn_conv_set_flags): bit 0 = nontemporal output
-// stores. Measured per conv in isolation 2-5 % faster (scripts/nt_ab.py: the once-written output
-// stays out of the L2 holding the k-loop's operand reuse), but no faster in the full step, where
-// the next layer reads that output; default off. Nontemporal LDS-DMA of the reused operands
-// was slower everywhere.
-__device__ int g_conv_flags = 0;
+// Nontemporal output stores / epilogue loads / operand DMA (scripts/nt_ab.py, runtime switches
+// in an earlier revision): 2-5 % per conv in isolation for nt stores, no gain in the full step
+// (the next layer reads the output), nt DMA of the reused operands slower everywhere -- and the
+// runtime branches alone cost ~1 % of the step. Plain stores / loads.
 
 __device__ __forceinline__ unsigned long long drn_realtime() {
   unsigned long long t;
@@ -253,12 +254,7 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
         }
         *reinterpret_cast<uint4*>(y + off) = pack8(f);
       } else {
-        if (g_conv_flags & 1) {
-          const u32x4_t ov = {o.x, o.y, o.z, o.w};
-          __builtin_nontemporal_store(ov, reinterpret_cast<u32x4_t*>(y + off));
-        } else {
-          *reinterpret_cast<uint4*>(y + off) = o;
-        }
+        *reinterpret_cast<uint4*>(y + off) = o;
         if (a.out_fill && a.out_stride > 1) {
           // zeros at this pixel's sibling phase positions (single-phase strided output)
           const int m = m0 + row;
@@ -610,9 +606,11 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
 
   extern __shared__ __attribute__((aligned(1024))) char smem[];
 
+#ifdef DRN_CONV_TRACE
   unsigned long long* const trace = g_conv_trace;
   unsigned long long t_start = 0;
   if (trace != nullptr) t_start = drn_realtime();
+#endif
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -886,10 +884,13 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
     asm volatile("" ::: "memory");
   }
   __syncthreads();  // all fragment reads done before the epilogue reuses the LDS
+#ifdef DRN_CONV_TRACE
   unsigned long long t_loop = 0;
   if (trace != nullptr) t_loop = drn_realtime();
+#endif
   // (the launcher sizes the dynamic LDS for max(NS * STAGE, BP * BC * 4))
   conv_epilogue<BP, BC, WP, WC, MI, MJ, NT, PF>(a, smem, acc, wp, wc, m0, c0, M, epre);
+#ifdef DRN_CONV_TRACE
   if (trace != nullptr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -903,6 +904,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
       r[3] = ((unsigned long long)xcc << 32) | hw;
     }
   }
+#endif
 }
 
 // largest grid that finalizes its input BatchNorm in the prologue (DRN_CFIN_MAX_BLOCKS)
@@ -1120,14 +1122,12 @@ DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
   return drn_conv_fwd(a, s);
 }
 
+#ifdef DRN_CONV_TRACE
 // diagnostics: per-workgroup timeline buffer for the LDS-DMA conv kernel (nullptr disables)
 DRN_API int drn_conv_trace_set(unsigned long long* buf) {
   return (int)hipMemcpyToSymbol(HIP_SYMBOL(drn::g_conv_trace), &buf, sizeof(buf));
 }
-
-DRN_API int drn_conv_set_flags(int flags) {
-  return (int)hipMemcpyToSymbol(HIP_SYMBOL(drn::g_conv_flags), &flags, sizeof(flags));
-}
+#endif
 
 DRN_API int drn_conv_glds_cfg_bp(int cfg) { return drn::glds_cfg_bp(cfg); }
 DRN_API int drn_conv_glds_num_cfgs() { return DRN_GLDS_NCFG + drn_conv_mt_num_cfgs(); }

@@ -234,9 +234,6 @@ class HipBackend(_Common):
         forced = os.environ.get("DRN_WGRAD_NS")
         self.forced_wgrad_ns = int(forced) if forced not in (None, "") else None
         self.tune_log: list = []
-        flags = os.environ.get("DRN_CONV_FLAGS")  # conv cache-policy switches (conv_fwd.hip g_conv_flags)
-        if flags not in (None, ""):
-            _lib.check(self.L.drn_conv_set_flags(int(flags)), "drn_conv_set_flags")
 
     def stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream

@@ -53,8 +53,11 @@ def _compile(src: Path, extra: list[str]) -> Path:
     obj = OBJ_DIR / (src.stem + ".o")
     if obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, _headers_mtime()):
         return obj
+    # DRN_CONV_TRACE=1: diagnostics build with the per-workgroup conv timeline
+    # (scripts/trace_conv.py); never the default -- the instrumentation costs ~2.5 % of a step
+    trace = ["-DDRN_CONV_TRACE"] if os.environ.get("DRN_CONV_TRACE") == "1" else []
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-I", str(INCLUDE),
-           "-Wno-unused-result", "-c", str(src), "-o", str(obj)] + extra
+           "-Wno-unused-result", "-c", str(src), "-o", str(obj)] + trace + extra
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{res.stderr[-6000:]}")

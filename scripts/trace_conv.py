@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-workgroup timeline of one LDS-DMA conv launch (drn_conv_trace_set): kernel span, block
 lifetime split (prologue+main loop / epilogue), blocks resident per CU over time.
-usage: trace_conv.py H C K R stride cfg [flags: pro res stats]"""
+usage: trace_conv.py H C K R stride cfg [flags: pro res stats]
+(needs the diagnostics build: DRN_CONV_TRACE=1 python -m distributed_resnet_tensorflow_amd.ops.build)"""
 import ctypes
 import os
 import sys
@@ -62,3 +63,6 @@ print("  resident blocks/CU over time: " + " ".join(f"{r:.1f}" for r in res))
 # start-time histogram (rounds)
 hist, edges = np.histogram(s, bins=20)
 print("  start histogram: " + " ".join(str(h) for h in hist) + f"  (bin {edges[1]:.1f} us)")
+bidx = np.nonzero(buf.view(-1, 4).cpu().numpy()[:, 0])[0]
+match = float(np.mean((bidx % 8) == xcc))
+print(f"  blocks whose XCC == blockIdx % 8: {match * 100:.1f}%   XCC histogram: {np.bincount(xcc, minlength=8).tolist()}")
