@@ -204,4 +204,7 @@ struct DrnConvWgradArgs {
   // Optional fused BatchNorm-backward dY (see DrnConvFwdArgs::bnb_x): dY_eff = A*dy + B*bnb_x + D
   const void* bnb_x;
   DrnBnFin bnb_fin;
+  // 1: every split adds its tile into out = the final, pre-zeroed gradient with fp32 atomics
+  // (no partial slabs, no drn_splitk_reduce)
+  int32_t atomic_out;
 };

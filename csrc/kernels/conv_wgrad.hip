@@ -51,6 +51,33 @@ __device__ __forceinline__ s16x4v tr_read(const char* base, int byte_off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + byte_off));
 }
 
+// Weight-gradient tile out: the split's fp32 partial slab (reduced by drn_splitk_reduce), or with
+// atomic_out the fp32 adds straight into the (pre-zeroed) gradient -- no slab, no reduce
+// launch; for layers with few weights (CIFAR) the reduce launch costs more than the atomics.
+// Not bitwise reproducible across runs (the deterministic mode never selects it).
+template <int MI, int MJ>
+__device__ __forceinline__ void wgrad_store(const DrnConvWgradArgs& a, f32x4_t (&acc)[MI][MJ], int split, int cb,
+                                            int kb, int Ktot, int lane) {
+  float* out = a.out + (a.atomic_out ? (size_t)0 : (size_t)split * a.K * Ktot);
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) {
+      const int co = cb + 16 * j + (lane & 15);
+      const int kr = kb + 16 * i + 4 * (lane >> 4);
+      if (co < a.K && kr < Ktot) {
+        float* p = out + (size_t)co * Ktot + kr;
+        if (a.atomic_out) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            __hip_atomic_fetch_add(p + e, acc[i][j][e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          *reinterpret_cast<f32x4_t*>(p) = acc[i][j];
+        }
+      }
+    }
+}
+
 template <int BKK, int BCO, bool PRO, int NST>
 __global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_wgrad_kernel(DrnConvWgradArgs a) {
   constexpr int BP = 64;                 // pixels per step
@@ -217,15 +244,7 @@ __global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_wgrad_kernel(DrnCo
     __syncthreads();
   }
 
-  float* out = a.out + (size_t)split * a.K * Ktot;
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < MJ; ++j) {
-      const int co = c0 + wc * WCO + 16 * j + (lane & 15);
-      const int kr = k0 + wk * WKK + 16 * i + 4 * (lane >> 4);
-      if (co < a.K && kr < Ktot) *reinterpret_cast<f32x4_t*>(out + (size_t)co * Ktot + kr) = acc[i][j];
-    }
+  wgrad_store<MI, MJ>(a, acc, split, c0 + wc * WCO, k0 + wk * WKK, Ktot, lane);
 }
 
 template <int BKK, int BCO, bool PRO>
@@ -596,15 +615,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
     asm volatile("" ::: "memory");
   }
 
-  float* out = a.out + (size_t)split * a.K * Ktot;
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < MJ; ++j) {
-      const int co = c0 + wc * WCO + 16 * j + (lane & 15);
-      const int kr = k0 + wk * WKK + 16 * i + 4 * (lane >> 4);
-      if (co < a.K && kr < Ktot) *reinterpret_cast<f32x4_t*>(out + (size_t)co * Ktot + kr) = acc[i][j];
-    }
+  wgrad_store<MI, MJ>(a, acc, split, c0 + wc * WCO, k0 + wk * WKK, Ktot, lane);
 }
 
 template <int BKK, int BCO, int NS, int BP, bool PRO, bool BNB = false>

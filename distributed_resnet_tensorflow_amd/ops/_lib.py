@@ -73,7 +73,7 @@ class DrnConvWgradArgs(ctypes.Structure):
         ("N", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("K", c_int), ("R", c_int), ("S", c_int),
         ("P", c_int), ("Q", c_int), ("stride", c_int), ("pad_h", c_int), ("pad_w", c_int), ("relu_in", c_int),
         ("splits", c_int), ("pix_per_split", c_int), ("fd_pq", DrnFastDiv), ("fd_q", DrnFastDiv),
-        ("bnb_x", c_p), ("bnb_fin", DrnBnFin),
+        ("bnb_x", c_p), ("bnb_fin", DrnBnFin), ("atomic_out", c_int),
     ]
 
 

@@ -231,6 +231,11 @@ class HipBackend(_Common):
         self.forced_cfg = int(forced) if forced not in (None, "") else None
         self.autotune = os.environ.get("DRN_AUTOTUNE", "1") == "1"
         self.wgrad_ns: dict = {}
+        # split-K by fp32 atomics into the gradient is a tuner candidate only once the executor
+        # guarantees zeroed gradients at the start of every backward (wgrad_atomic_ok); it sets
+        # wgrad_atomic_used when some layer picked it
+        self.wgrad_atomic_ok = False
+        self.wgrad_atomic_used = False
         forced = os.environ.get("DRN_WGRAD_NS")
         self.forced_wgrad_ns = int(forced) if forced not in (None, "") else None
         self.tune_log: list = []
@@ -404,7 +409,7 @@ class HipBackend(_Common):
     WGRAD_TARGETS = tuple(int(v) for v in os.environ.get("DRN_WGRAD_TARGETS", "128,256,512").split(","))
 
     def wgrad_args(self, x, dy, out, g: ConvGeom, in_bn=None, relu_in=True, ws=None, target_blocks: int = 0,
-                   bnb=None):
+                   bnb=None, atomic: bool = False):
         N, H, W, C = x.shape
         N2, P, Q, K = dy.shape
         Kd, R, S, Cd = out.shape
@@ -428,8 +433,9 @@ class HipBackend(_Common):
             f = bf.struct()
             f.publish = 0  # the data-gradient consumer publishes dgamma / dbeta
             a.bnb_fin = f
-        if splits == 1:
+        if splits == 1 or atomic:
             a.out = out.data_ptr()
+            a.atomic_out = 1 if (atomic and splits > 1) else 0
         else:
             need = splits * out.numel()
             assert ws is not None and ws.numel() >= need, f"wgrad workspace too small ({need})"
@@ -455,7 +461,7 @@ class HipBackend(_Common):
 
     def _wgrad_full(self, a, ns: int, out, st):
         self._wgrad_kernel(a, ns, st)
-        if a.splits > 1:
+        if a.splits > 1 and not a.atomic_out:
             _lib.check(self.L.drn_splitk_reduce(a.out, out.data_ptr(), out.numel(), a.splits, 1.0, 0, st),
                        "drn_splitk_reduce")
 
@@ -466,14 +472,15 @@ class HipBackend(_Common):
         real launch that follows)."""
         st = self.stream()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        best, best_t = (0, 2), float("inf")
+        best, best_t = (0, 2, False), float("inf")
         cands = tuple(int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6").split(","))
         seen = set()
-        for tgt in self.WGRAD_TARGETS:
-            a = args_for(tgt)
-            if a.splits in seen:
+        modes = (False, True) if self.wgrad_atomic_ok else (False,)
+        for tgt, atomic in [(t, m) for t in self.WGRAD_TARGETS for m in modes]:
+            a = args_for(tgt, atomic)
+            if (a.splits, a.atomic_out) in seen:
                 continue
-            seen.add(a.splits)
+            seen.add((a.splits, a.atomic_out))
             for ns in cands:
                 if self.L.drn_conv_wgrad2(ctypes.byref(a), self.zero_page.data_ptr(), ns, st) != 0:
                     continue  # pipeline not available for this launch (e.g. BN-backward dY: LDS-DMA only)
@@ -486,12 +493,14 @@ class HipBackend(_Common):
                 ev1.synchronize()
                 ms = ev0.elapsed_time(ev1) / iters
                 if ms < best_t:
-                    best, best_t = (tgt, ns), ms
+                    best, best_t = (tgt, ns, bool(a.atomic_out)), ms
+        if best[2]:
+            self.wgrad_atomic_used = True  # the executor now zeroes the gradients every step
         self.tune_log.append((("wgrad",) + key, best, round(best_t * 1e3, 1)))
         return best
 
     def conv_wgrad(self, x, dy, out, g, in_bn=None, relu_in=True, ws=None, bnb=None):
-        args_for = lambda tgt: self.wgrad_args(x, dy, out, g, in_bn, relu_in, ws, tgt, bnb)
+        args_for = lambda tgt, atomic=False: self.wgrad_args(x, dy, out, g, in_bn, relu_in, ws, tgt, bnb, atomic)
         a = args_for(0)
         st = self.stream()
         if self.forced_wgrad_ns is not None:
@@ -500,11 +509,13 @@ class HipBackend(_Common):
         key = self.wgrad_key(a)
         if key not in self.wgrad_ns and self.autotune and not torch.cuda.is_current_stream_capturing():
             self.wgrad_ns[key] = self._tune_wgrad(args_for, out, key)
-        tgt, ns = self.wgrad_ns.get(key, (0, 2))
+            if self.wgrad_ns[key][2]:
+                self.zero_(out)  # the timing launches left partial sums in this gradient slot
+        tgt, ns, atomic = self.wgrad_ns.get(key, (0, 2, False))
         if ns == 0 and a.bnb_x is not None:
             ns = 2
-        if tgt:
-            a = args_for(tgt)
+        if tgt or atomic:
+            a = args_for(tgt, atomic)
         self._wgrad_full(a, ns, out, st)
 
     # -- batch norm -----------------------------------------------------------------------------

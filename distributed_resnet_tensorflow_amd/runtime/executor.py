@@ -117,6 +117,12 @@ class Executor:
         # (ResNet-50 bs128, scripts/op_breakdown.py: applies -330 us, consumers +800 us; step
         # 10.74 -> 11.18 ms)
         self.fuse_bnb = os.environ.get("DRN_FUSE_BNB", "0") == "1"
+        # split-K weight gradients may accumulate with fp32 atomics (the autotuner's choice per
+        # layer; the gradients are then zeroed at the start of every backward); not in the
+        # bitwise-reproducible mode
+        if hasattr(backend, "wgrad_atomic_ok"):
+            backend.wgrad_atomic_ok = os.environ.get("DRN_WGRAD_ATOMIC", "1") == "1" and \
+                os.environ.get("DRN_DETERMINISTIC", "0") != "1"
         # debug mode: synchronous finiteness checks after every block (forward and backward)
         self.check_nan = os.environ.get("DRN_CHECK_NAN", "0") == "1"
         # deterministic mode (DRN_DETERMINISTIC=1): bitwise-reproducible steps -- one statistics
@@ -609,6 +615,9 @@ class Executor:
     def backward(self):
         be, sp = self.be, self.spec
         N, C, ncls = self.N, sp.final_c, sp.num_classes
+        if getattr(be, "wgrad_atomic_used", False):
+            # weight gradients of layers whose split-K partials are added with atomics
+            be.zero_(self.P.grad)
         # dense layer: its weight / bias gradients only feed the optimizer, so with the side
         # stream they run there, off the data-gradient chain
         if self.side is not None:

@@ -709,3 +709,24 @@ def test_wgrad_bnb_prologue(hip, ref, ns, pro):
     hip._wgrad_full(a, ns, dw, hip.stream())
     torch.cuda.synchronize()
     assert rel(dw, dw_ref) < 2e-2, ns
+
+
+@pytest.mark.parametrize("case", [(4, 16, 16, 16, 3, 1, 1), (4, 24, 64, 32, 1, 1, 0), (4, 33, 32, 64, 3, 2, 1)])
+@pytest.mark.parametrize("ns", [0, 2, 5])
+def test_wgrad_atomic_split_k(hip, ref, case, ns):
+    """Split-K weight gradient accumulated with fp32 atomics straight into the (pre-zeroed)
+    gradient instead of partial slabs + drn_splitk_reduce."""
+    N, H, C, K, R, s, p = case
+    torch.manual_seed(31 + ns)
+    P = (H + 2 * p - R) // s + 1
+    x = bf(torch.randn(N, H, H, C))
+    dy = bf(torch.randn(N, P, P, K))
+    g = ConvGeom(s, p, p)
+    dw_ref = torch.zeros(K, R, R, C)
+    ref.conv_wgrad(x.float(), dy.float(), dw_ref, g)
+    dw = torch.zeros(K, R, R, C, device="cuda")
+    a = hip.wgrad_args(x.cuda(), dy.cuda(), dw, g, target_blocks=4096, atomic=True)
+    assert a.splits > 1 and a.atomic_out == 1
+    hip._wgrad_full(a, ns, dw, hip.stream())
+    torch.cuda.synchronize()
+    assert rel(dw, dw_ref) < 1e-2
