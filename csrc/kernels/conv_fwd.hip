@@ -549,6 +549,31 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// Order of the k-stages (tap r, tap s, channel chunk ci) of the LDS-DMA kernels: taps outer,
+// channel chunks inner (KRSC order). -DDRN_KORDER_CHUNK_OUTER fetches the R*S shifted windows
+// of one channel chunk in consecutive stages instead (shorter L2 reuse distance); measured
+// identical on every ResNet-50 3x3 layer and on the step (profiles/r2_experiments.md).
+template <int BK>
+__device__ __forceinline__ void kstep_next(int& r, int& s, int& ci, int R, int S, int C) {
+#ifndef DRN_KORDER_CHUNK_OUTER
+  if ((ci += BK) == C) {
+    ci = 0;
+    if (++s == S) {
+      s = 0;
+      ++r;
+    }
+  }
+#else
+  if (++s == S) {
+    s = 0;
+    if (++r == R) {
+      r = 0;
+      ci += BK;
+    }
+  }
+#endif
+}
+
 // BK = 64: 128-byte LDS rows, slot(chunk c of row r) = c ^ ((r >> 1) & 7)
 // BK = 32: 64-byte LDS rows (a stage holds one 32-deep MFMA k-slice; twice the stages in the same
 //          LDS, i.e. a deeper pipeline), slot = c ^ (((r >> 2) & 1) << 1); both conflict-free for
@@ -705,15 +730,8 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
         glds16(src, st + (BC + BP + RPG * NW * i + RPG * wave) * ROWB);
       }
     }
-    ik += BK;
-    ici += BK;
-    if (ici == C) {
-      ici = 0;
-      if (++is == a.S) {
-        is = 0;
-        ++ir;
-      }
-    }
+    kstep_next<BK>(ir, is, ici, a.R, a.S, C);
+    ik = (ir * a.S + is) * C + ici;
   };
 
   const int wp = wave % WAVES_P;
@@ -816,13 +834,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
         lds_write16(pa[i], o);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if ((xci += BK) == C) {
-        xci = 0;
-        if (++xs == a.S) {
-          xs = 0;
-          ++xr;
-        }
-      }
+      kstep_next<BK>(xr, xs, xci, a.R, a.S, C);
     }
     if constexpr (PRO) {
       char* sw = smem + (t % NS) * STAGE;
@@ -853,15 +865,8 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
         sh2[2 * q + 1] = f32x2_t{__uint_as_float(v[GB + 2 + q][2]), __uint_as_float(v[GB + 2 + q][3])};
       }
       lds_bn_relu_store<GB, true>(pa, v, ok, sc2, sh2);
-      if (SROW) {
-        ++xr;
-      } else if ((xci += BK) == C) {
-        xci = 0;
-        if (++xs == a.S) {
-          xs = 0;
-          ++xr;
-        }
-      }
+      if (SROW) ++xr;
+      else kstep_next<BK>(xr, xs, xci, a.R, a.S, C);
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");

@@ -56,6 +56,7 @@ def _compile(src: Path, extra: list[str]) -> Path:
     # DRN_CONV_TRACE=1: diagnostics build with the per-workgroup conv timeline
     # (scripts/trace_conv.py); never the default -- the instrumentation costs ~2.5 % of a step
     trace = ["-DDRN_CONV_TRACE"] if os.environ.get("DRN_CONV_TRACE") == "1" else []
+    trace += os.environ.get("DRN_HIPCC_EXTRA", "").split()  # A/B builds (e.g. -DDRN_KORDER_TAP_OUTER)
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-I", str(INCLUDE),
            "-Wno-unused-result", "-c", str(src), "-o", str(obj)] + trace + extra
     res = subprocess.run(cmd, capture_output=True, text=True)
