@@ -111,7 +111,7 @@ def main():
         ex.forward(train=True)
         if eng is not None:
             eng.begin_step()
-        ex.backward()
+        ex.backward(defer_tail=eng is None)
         if eng is not None:
             eng.apply_gradients(eng.finish(), 1.0 / world)
         else:

@@ -13,6 +13,8 @@ namespace drn {
 // reduces the per-channel sum / sum of squares of its bf16-rounded outputs -- the batch
 // statistics of the first block's BatchNorm -- into replica blockIdx % rep (bn_stats_kernel's
 // pattern), which saves the separate statistics pass over the pooled tensor.
+// KC > 0: the window size is the compile-time KC (the ImageNet stem's 3x3), taps fully unrolled.
+template <int KC>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
                                                           uint8_t* __restrict__ arg, int N, int H, int W, int C, int P,
                                                           int Q, int k, int stride, int pad_h, int pad_w,
@@ -35,17 +37,41 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restri
         uint8_t bi[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; bi[j] = 0; }
-        for (int r = 0; r < k; ++r) {
-          const int h = p * stride - pad_h + r;
-          if (h < 0 || h >= H) continue;
-          for (int t = 0; t < k; ++t) {
-            const int w = q * stride - pad_w + t;
-            if (w < 0 || w >= W) continue;
+        if constexpr (KC > 0) {
+          // fixed window: all KC*KC taps in flight together (out-of-image taps read as -inf and,
+          // with the strict '>', never win -- the same first-maximum rule as the generic loop)
+          uint4 v[KC * KC];
+          const uint32_t ninf = 0xFF80FF80u;
+#pragma unroll
+          for (int r = 0; r < KC; ++r)
+#pragma unroll
+            for (int t = 0; t < KC; ++t) {
+              const int h = p * stride - pad_h + r, w = q * stride - pad_w + t;
+              v[r * KC + t] = ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W)
+                                  ? *reinterpret_cast<const uint4*>(x + (((size_t)n * H + h) * W + w) * C + cv * 8)
+                                  : make_uint4(ninf, ninf, ninf, ninf);
+            }
+#pragma unroll
+          for (int tp = 0; tp < KC * KC; ++tp) {
             float f[8];
-            unpack8(*reinterpret_cast<const uint4*>(x + (((size_t)n * H + h) * W + w) * C + cv * 8), f);
+            unpack8(v[tp], f);
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-              if (f[j] > best[j]) { best[j] = f[j]; bi[j] = (uint8_t)(r * k + t); }
+              if (f[j] > best[j]) { best[j] = f[j]; bi[j] = (uint8_t)tp; }
+          }
+        } else {
+          for (int r = 0; r < k; ++r) {
+            const int h = p * stride - pad_h + r;
+            if (h < 0 || h >= H) continue;
+            for (int t = 0; t < k; ++t) {
+              const int w = q * stride - pad_w + t;
+              if (w < 0 || w >= W) continue;
+              float f[8];
+              unpack8(*reinterpret_cast<const uint4*>(x + (((size_t)n * H + h) * W + w) * C + cv * 8), f);
+#pragma unroll
+              for (int j = 0; j < 8; ++j)
+                if (f[j] > best[j]) { best[j] = f[j]; bi[j] = (uint8_t)(r * k + t); }
+            }
           }
         }
         const size_t o = ((size_t)row * Q + q) * CV + cv;
@@ -130,6 +156,8 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restri
 // windows touching the block are each read once (dy + argmax) and scattered to the block's 4
 // pixels in registers -- every window record is read ~1x instead of ~2.25x, and no thread loops
 // over a data-dependent window count.
+// NWD = max windows per dimension over a 2x2 input block: 2 for k <= 3, 3 for k = 4.
+template <int NWD>
 __global__ __launch_bounds__(256) void maxpool_bwd_s2_kernel(const bf16_t* __restrict__ dy,
                                                              const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx,
                                                              int N, int H, int W, int C, int P, int Q, int k,
@@ -158,12 +186,28 @@ __global__ __launch_bounds__(256) void maxpool_bwd_s2_kernel(const bf16_t* __res
       // (p_lo = ceil((h0 + pad - k + 1) / 2); C's truncation only matters below 0, where max() clamps)
       const int p_lo = max(0, (h0 + pad_h - k + 2) / 2), p_hi = min(P - 1, (h0 + 1 + pad_h) / 2);
       const int q_lo = max(0, (w0 + pad_w - k + 2) / 2), q_hi = min(Q - 1, (w0 + 1 + pad_w) / 2);
-      for (int p = p_lo; p <= p_hi; ++p) {
-        for (int q = q_lo; q <= q_hi; ++q) {
-          const size_t o = (((size_t)n * P + p) * Q + q) * CV + cv;
-          const uint2 ar = reinterpret_cast<const uint2*>(arg)[o];
+      // at most NWD windows per dimension touch a 2x2 block: all their records in flight together
+      uint4 gv[NWD][NWD];
+      uint2 av[NWD][NWD];
+#pragma unroll
+      for (int pi = 0; pi < NWD; ++pi)
+#pragma unroll
+        for (int qi = 0; qi < NWD; ++qi) {
+          const int p = p_lo + pi, q = q_lo + qi;
+          const bool ok = p <= p_hi && q <= q_hi;
+          const size_t o = (((size_t)n * P + (ok ? p : 0)) * Q + (ok ? q : 0)) * CV + cv;
+          gv[pi][qi] = ok ? reinterpret_cast<const uint4*>(dy)[o] : make_uint4(0u, 0u, 0u, 0u);
+          av[pi][qi] = ok ? reinterpret_cast<const uint2*>(arg)[o] : make_uint2(~0u, ~0u);  // tap 255: never
+        }
+#pragma unroll
+      for (int pi = 0; pi < NWD; ++pi) {
+        const int p = p_lo + pi;
+#pragma unroll
+        for (int qi = 0; qi < NWD; ++qi) {
+          const int q = q_lo + qi;
+          const uint2 ar = av[pi][qi];
           float g[8];
-          unpack8(reinterpret_cast<const uint4*>(dy)[o], g);
+          unpack8(gv[pi][qi], g);
           const uint8_t bt[8] = {(uint8_t)(ar.x), (uint8_t)(ar.x >> 8), (uint8_t)(ar.x >> 16), (uint8_t)(ar.x >> 24),
                                  (uint8_t)(ar.y), (uint8_t)(ar.y >> 8), (uint8_t)(ar.y >> 16), (uint8_t)(ar.y >> 24)};
           const int r0 = h0 - (2 * p - pad_h), s0 = w0 - (2 * q - pad_w);
@@ -204,8 +248,9 @@ DRN_API int drn_maxpool_fwd(const void* x, void* y, uint8_t* arg, int N, int H, 
   if (C % 8 || C / 8 > 256 || (part != nullptr && rep < 1)) return (int)hipErrorInvalidValue;
   const int rows = N * P;
   const int rpb = rows >= 4096 ? 4 : 1;  // ~1.8K blocks at the ImageNet stem (128 x 56 rows)
-  hipLaunchKernelGGL(drn::maxpool_fwd_kernel, dim3((rows + rpb - 1) / rpb), dim3(256), part ? 256 * 17 * 4 : 0, s,
-                     (const bf16_t*)x, (bf16_t*)y, arg, N, H, W, C, P, Q, k, stride, pad_h, pad_w, rpb, part, rep);
+  auto kern = k == 3 ? drn::maxpool_fwd_kernel<3> : drn::maxpool_fwd_kernel<0>;
+  hipLaunchKernelGGL(kern, dim3((rows + rpb - 1) / rpb), dim3(256), part ? 256 * 17 * 4 : 0, s, (const bf16_t*)x,
+                     (bf16_t*)y, arg, N, H, W, C, P, Q, k, stride, pad_h, pad_w, rpb, part, rep);
   return (int)hipGetLastError();
 }
 
@@ -215,8 +260,9 @@ DRN_API int drn_maxpool_bwd(const void* dy, const uint8_t* arg, void* dx, int N,
   if (stride == 2 && k <= 4 && C / 8 <= 256) {
     const int rows = N * ((H + 1) / 2);
     const int rpb = rows >= 4096 ? 4 : 1;
-    hipLaunchKernelGGL(drn::maxpool_bwd_s2_kernel, dim3((rows + rpb - 1) / rpb), dim3(256), 0, s, (const bf16_t*)dy,
-                       arg, (bf16_t*)dx, N, H, W, C, P, Q, k, pad_h, pad_w, rpb);
+    auto kern = k <= 3 ? drn::maxpool_bwd_s2_kernel<2> : drn::maxpool_bwd_s2_kernel<3>;
+    hipLaunchKernelGGL(kern, dim3((rows + rpb - 1) / rpb), dim3(256), 0, s, (const bf16_t*)dy, arg, (bf16_t*)dx, N,
+                       H, W, C, P, Q, k, pad_h, pad_w, rpb);
     return (int)hipGetLastError();
   }
   const int64_t total = (int64_t)N * H * W * (C / 8);

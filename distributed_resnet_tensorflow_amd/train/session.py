@@ -128,7 +128,7 @@ class TrainingSession:
             g = self.engine.finish()
             self.engine.apply_gradients(g, 1.0 / self.world)
         else:
-            ex.backward()
+            ex.backward(defer_tail=not ex.check_nan)
             ex.apply_gradients()
 
     def step(self):

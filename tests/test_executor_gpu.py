@@ -164,6 +164,37 @@ def test_deterministic_mode_is_bitwise_reproducible(monkeypatch):
         assert torch.equal(a, b)
 
 
+def test_deferred_stem_gradient_matches_joined_step(monkeypatch):
+    """backward(defer_tail=True): the optimizer updates every parameter but the stem's while the
+    stem's weight gradient still runs on the side stream, then joins and updates the stem. Eager
+    and HIP-graph-replayed deferred steps are bitwise equal to the fully joined step
+    (deterministic mode: no atomics anywhere)."""
+    from distributed_resnet_tensorflow_amd.runtime.graph import StepGraph
+    monkeypatch.setenv("DRN_DETERMINISTIC", "1")
+    spec, N = cifar_resnet_v2(14), 16
+    outs = []
+    for mode in ("joined", "deferred", "graph"):
+        ex = Executor(spec, N, HipBackend(), "cuda", seed=3)
+        assert ex._stem_hi == ex.stem_op.dw.numel() and ex.side is not None
+        g = torch.Generator().manual_seed(9)
+        ex.images.zero_()
+        ex.images[..., :3] = torch.randn(N, 32, 32, 3, generator=g).bfloat16().cuda()
+        ex.labels.copy_(torch.randint(0, 10, (N,), generator=g, dtype=torch.int32))
+        ex.set_lr(0.1)
+        fn = lambda: (ex.forward(True), ex.backward(defer_tail=mode != "joined"), ex.apply_gradients())
+        if mode == "graph":
+            gr = StepGraph(fn, warmup=2)
+            gr.replay()
+        else:
+            for _ in range(3):
+                fn()
+        torch.cuda.synchronize()
+        outs.append((ex.P.master.clone(), ex.P.momentum.clone(), ex.P.bn_state.clone()))
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
+
+
 def test_precision_fp32_reference_backend_on_gpu():
     """--precision=fp32: the executor runs the fp32 PyTorch reference backend on the GPU device
     (debug path) and its step agrees with the bf16 HIP step to bf16 tolerance."""
