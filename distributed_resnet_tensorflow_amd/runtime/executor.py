@@ -330,6 +330,13 @@ class Executor:
         # the stem's weights lead the flat parameter buffer: [0, _stem_hi) is the slice the
         # optimizer updates last when backward(defer_tail=True) (0: layout differs, no deferral)
         self._stem_hi = int(self.stem_op.dw.numel()) if self.stem_op.grad_lo == 0 else 0
+        # DRN_DEFER_TAIL=auto: only where the stem's weight gradient is long enough to hide the
+        # optimizer (ImageNet: 40 G MAC, ~0.2 ms); a CIFAR stem's is microseconds and the split
+        # update only adds a launch to its launch-bound graph
+        stem_macs = N * sp.stem_hw * sp.stem_hw * sp.stem.cout * sp.stem.k * sp.stem.k * sp.stem.cin_store
+        mode = os.environ.get("DRN_DEFER_TAIL", "auto")
+        if mode == "0" or (mode == "auto" and stem_macs < 1e9):
+            self._stem_hi = 0
         self._tail_ev = None
         img = sp.image_size
         self.images = self._act(N, img, img, sp.stem.cin_store)

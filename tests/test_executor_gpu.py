@@ -171,6 +171,7 @@ def test_deferred_stem_gradient_matches_joined_step(monkeypatch):
     (deterministic mode: no atomics anywhere)."""
     from distributed_resnet_tensorflow_amd.runtime.graph import StepGraph
     monkeypatch.setenv("DRN_DETERMINISTIC", "1")
+    monkeypatch.setenv("DRN_DEFER_TAIL", "1")  # (auto defers only long stem gradients: ImageNet)
     spec, N = cifar_resnet_v2(14), 16
     outs = []
     for mode in ("joined", "deferred", "graph"):
