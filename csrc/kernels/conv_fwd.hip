@@ -691,17 +691,23 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   auto issue = [&](int slot) {
     char* st = smem + slot * STAGE;
     if constexpr (SROW) {  // stage = filter row ir; chunk lc = (tap lc*8/C, channels (lc*8)%C)
+      // (C == 4, packed stem: stage = filter rows 2ir, 2ir+1, chunks 0-3 / 4-7 = their 4 tap pairs)
       const int SC = a.S * C;
+      const int rps = C == 4 ? 2 : 1;
 #pragma unroll
       for (int i = 0; i < GA; ++i) {
-        const void* src = (wsrc[i] && alc[i] * 8 < SC) ? (const void*)(wsrc[i] + ir * SC + alc[i] * 8) : zero;
+        const int sub = rps == 2 ? alc[i] >> 2 : 0, lc = rps == 2 ? alc[i] & 3 : alc[i];
+        const int row = ir * rps + sub;
+        const void* src = (wsrc[i] && lc * 8 < SC && row < a.R) ? (const void*)(wsrc[i] + row * SC + lc * 8) : zero;
         glds16(src, st + (RPG * NW * i + RPG * wave) * ROWB);
       }
 #pragma unroll
       for (int i = 0; i < GB; ++i) {
-        const int h = bh[i] + ir, w = bw[i] + blc[i] * 8 / C;
-        const bool ok = blc[i] * 8 < SC && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-        const void* src = ok ? (const void*)(xg + (boff[i] + ir * a.W * C + blc[i] * 8)) : zero;
+        const int sub = rps == 2 ? blc[i] >> 2 : 0, lc = rps == 2 ? blc[i] & 3 : blc[i];
+        const int row = ir * rps + sub;
+        const int h = bh[i] + row, w = bw[i] + lc * 8 / C;
+        const bool ok = lc * 8 < SC && row < a.R && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+        const void* src = ok ? (const void*)(xg + (boff[i] + row * a.W * C + lc * 8)) : zero;
         glds16(src, st + (BC + RPG * NW * i + RPG * wave) * ROWB);
       }
       ++ir;
@@ -751,7 +757,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   for (int j = 0; j < MJ; ++j) boffl[j] = (BC + wp * WP + j * 16 + fr) * ROWB;
   const int swz = glds_swz<BK>(fr);  // fragment row groups are 16-aligned: the swizzle bits are fr's
 
-  const int T = SROW ? a.R : Ktot / BK;
+  const int T = SROW ? (C == 4 ? (a.R + 1) / 2 : a.R) : Ktot / BK;
   // fused-BN operands: [scale C][shift C] fp32 behind the stages, written AFTER the first
   // pipeline stages are issued (their LDS-DMA latency covers the parameter loads / finalize)
   // (behind the stages actually used: a convolution with fewer k-stages than NS - e.g. a 1x1
@@ -924,7 +930,8 @@ static int cfin_max_blocks() {
 
 template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF, int BK, bool PRO, bool SROW = false, bool BNB = false>
 static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
-  const int T = a->C == 8 || a->C == 16 ? a->R : (a->R * a->S * a->C) / BK;  // k-stages (SROW: filter rows)
+  const int T = a->C == 4 ? (a->R + 1) / 2 : a->C == 8 || a->C == 16 ? a->R : (a->R * a->S * a->C) / BK;  // k-stages
+                                                          // (SROW: filter rows; packed stem: row pairs)
   const int LDS0 = (T < NS ? T : NS) * (BC + BP * (BNB ? 2 : 1)) * BK * 2;  // stage slots actually used
   const int lds_main = LDS0 + (PRO ? 8 * a->C : 0) + (BNB ? 12 * a->C : 0);  // + fused-BN parameters
   const int LDS = lds_main > BP * BC * 4 ? lds_main : BP * BC * 4;  // epilogue staging tile
@@ -959,9 +966,10 @@ static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t 
 template <int BP, int BC, int WAVES_P, int NS, int NW = 4, int BK = 64>
 static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
   const bool pf = a->residual != nullptr || a->bn_x != nullptr;
-  if (a->C == 8 || a->C == 16) {  // row-staged narrow conv (the stem, the CIFAR first stage)
+  if (a->C == 4 || a->C == 8 || a->C == 16) {  // row-staged narrow conv (the stem, the CIFAR first stage)
     if constexpr (BK == 64) {
-      if (a->S * a->C > 64) return (int)hipErrorInvalidValue;
+      if (a->S * a->C > (a->C == 4 ? 32 : 64)) return (int)hipErrorInvalidValue;
+      if (a->C == 4 && (a->S % 2 || a->in_scale != nullptr)) return (int)hipErrorInvalidValue;
       if (a->in_scale != nullptr)
         return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, true, true>(a, zero, stream)
                   : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, true, true>(a, zero, stream);
@@ -1042,7 +1050,7 @@ static int glds_cfg_bp(int cfg) {
 // 64 x 128 tiles once the 128 x 128 grid stops filling the chip.
 static int glds_default_cfg(const DrnConvFwdArgs* a) {
   const long M = (long)a->N * a->P * a->Q;
-  if (a->C == 8 || a->C == 16) return a->K <= 32 ? 23 : a->K <= 64 ? 3 : 0;  // row-staged: 64-deep stages
+  if (a->C == 4 || a->C == 8 || a->C == 16) return a->K <= 32 ? 23 : a->K <= 64 ? 3 : 0;  // row-staged
   if (a->C % 64) return 18;  // 32-channel inputs: the 32-deep-stage family
   auto blocks = [&](int bp, int bc) { return ((M + bp - 1) / bp) * ((a->K + bc - 1) / bc); };
   if (a->K <= 64) return blocks(256, 64) >= 384 ? 3 : 7;
@@ -1096,6 +1104,9 @@ DRN_API int drn_conv_mt_ok(const DrnConvFwdArgs* a);
 DRN_API int drn_conv_glds_ok(const DrnConvFwdArgs* a) {
   if (a->bnb_x != nullptr)  // fused BN-backward input: LDS-DMA 64-deep stages only
     return a->C % 64 == 0 && a->C <= 4096 && a->dil == 1 && a->in_scale == nullptr;
+  if (a->C == 4)  // packed stem (stem.hip): tap pairs of 4 channels, two filter rows per stage
+    return a->dil == 1 && a->S % 2 == 0 && a->S * a->C <= 32 && a->in_scale == nullptr && a->bn_x == nullptr &&
+           a->residual == nullptr;
   if (a->C == 8 || a->C == 16)  // row-staged narrow conv (stem, CIFAR stage 1)
     return a->dil == 1 && a->S * a->C <= 64 && (a->in_scale == nullptr || a->relu_in != 0);
   return a->C % 32 == 0 && a->dil == 1 && (a->in_scale == nullptr || (a->C <= 4096 && a->relu_in != 0));
@@ -1105,7 +1116,10 @@ DRN_API int drn_conv_glds_ok(const DrnConvFwdArgs* a) {
 // A consumer-side BN finalize (in_fin) runs only on the LDS-DMA path; on the register-staged
 // kernel the finalize is a separate launch ahead of the conv (drn_bn_finalize semantics).
 DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
-  if ((a->C % 8) != 0 || (a->K % 8) != 0) return (int)hipErrorInvalidValue;
+  if ((a->C % 8) != 0 && a->C != 4) return (int)hipErrorInvalidValue;
+  if ((a->K % 8) != 0) return (int)hipErrorInvalidValue;
+  if (a->C == 4 && (!drn_conv_glds_ok(a) || zero == nullptr || a->cfg == 100 || a->cfg >= DRN_GLDS_NCFG))
+    return (int)hipErrorInvalidValue;  // the packed stem exists on the one-tile LDS-DMA path only
   if (a->fin_cnt != nullptr && (a->stats == nullptr || a->K > 64 * 64)) return (int)hipErrorInvalidValue;
   if (a->in_fin.stats != nullptr &&
       (a->in_scale == nullptr || a->in_fin.C != a->C || a->in_fin.G < 1 || a->in_fin.G > DRN_BN_FIN_GMAX))

@@ -743,7 +743,11 @@ DRN_API int drn_conv_wgrad(DrnConvWgradArgs* a, hipStream_t s) {
 
 // LDS-DMA wgrad (no prologue); ns = pipeline stages (2 or 3), 0 = register-staged kernel.
 DRN_API int drn_conv_wgrad2(DrnConvWgradArgs* a, const void* zero, int ns, hipStream_t s) {
-  if ((a->C % 8) != 0 || (a->K % 8) != 0 || a->splits < 1 || (a->pix_per_split % 64) != 0)
+  // C == 4: the packed stem (stem.hip) -- every 16-byte k piece is a tap pair x 4 channels, so the
+  // tap count must be even (S padded to 8); LDS-DMA kernels, no fused prologue
+  const bool packed = a->C == 4 && a->S % 2 == 0 && a->in_scale == nullptr && a->bnb_x == nullptr && zero != nullptr &&
+                      ns != 0;
+  if (((a->C % 8) != 0 && !packed) || (a->K % 8) != 0 || a->splits < 1 || (a->pix_per_split % 64) != 0)
     return (int)hipErrorInvalidValue;
   // the LDS-DMA kernels' fused BN prologue always applies the ReLU (pre-activation v2)
   if (a->bnb_x != nullptr && (zero == nullptr || ns == 0 || (a->in_scale != nullptr && a->relu_in == 0)))

@@ -673,6 +673,28 @@ class HipBackend(_Common):
     def cast_bf16(self, x, y):
         _lib.check(self.L.drn_cast_bf16(x.data_ptr(), y.data_ptr(), x.numel(), self.stream()), "drn_cast_bf16")
 
+    # -- packed stem (csrc/kernels/stem.hip) ---------------------------------------------------------
+    def stem_pack_input(self, x, xp):
+        """x [N,H,W,8] bf16 -> xp [N,H,W+2,4] (pad columns zeroed once by the caller)."""
+        N, H, W, C = x.shape
+        assert C == 8 and tuple(xp.shape) == (N, H, W + 2, 4) and xp.is_contiguous() and x.is_contiguous()
+        _lib.check(self.L.drn_stem_pack_input(x.data_ptr(), xp.data_ptr(), N * H, W, self.stream()),
+                   "drn_stem_pack_input")
+
+    def stem_pack_weights(self, w, wp):
+        K, R, S, C = w.shape
+        K2, R2, S8, C4 = wp.shape
+        assert (K2, R2) == (K, R) and w.dtype == wp.dtype == torch.bfloat16
+        _lib.check(self.L.drn_stem_pack_weights(w.data_ptr(), wp.data_ptr(), K, R, S, C, S8, C4, self.stream()),
+                   "drn_stem_pack_weights")
+
+    def stem_unpack_grad(self, dwp, dw):
+        K, R, S, C = dw.shape
+        K2, R2, S8, C4 = dwp.shape
+        assert (K2, R2) == (K, R) and dw.dtype == dwp.dtype == torch.float32 and dw.is_contiguous()
+        _lib.check(self.L.drn_stem_unpack_grad(dwp.data_ptr(), dw.data_ptr(), K, R, S, C, S8, C4, self.stream()),
+                   "drn_stem_unpack_grad")
+
     def weight_tflip(self, wb, wt, table, ntab, total):
         _lib.check(self.L.drn_weight_tflip(wb.data_ptr(), wt.data_ptr(), table.data_ptr(), ntab, total,
                                            self.stream()), "drn_weight_tflip")

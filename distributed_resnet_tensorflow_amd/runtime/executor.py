@@ -340,6 +340,25 @@ class Executor:
         self._tail_ev = None
         img = sp.image_size
         self.images = self._act(N, img, img, sp.stem.cin_store)
+        # Packed stem (csrc/kernels/stem.hip, DRN_STEM_PACK=1 default on HIP): the 7x7/2 stem over
+        # RGB runs on a 4-channel copy of the images with a zero pixel column on each side and on
+        # weights padded to 8 taps per row, so one 16-byte piece is a tap PAIR: 4 forward k-stages
+        # instead of 7 and 2 weight-gradient k-tiles instead of 4 (62.5 % of the 8-channel
+        # reduction is zero padding). Checkpoint / optimizer layout is unchanged: the packed
+        # weights are derived after every update, the gradient mapped back after the wgrad.
+        c0 = sp.stem
+        self.stem_pack = (self.is_hip and os.environ.get("DRN_STEM_PACK", "1") == "1" and c0.k % 2 == 1
+                          and c0.stride == 2 and c0.cin <= 4 and c0.cin_store == 8 and img % 2 == 0)
+        if self.stem_pack:
+            s8 = c0.k + 1
+            n_xp = N * img * (img + 2) * 4
+            # + slack: a tap-pair piece at the last pad column reads 8 bytes past the last row
+            self._stem_xp_buf = torch.zeros(n_xp + 64, dtype=torch.bfloat16, device=self.device)
+            self.stem_xp = self._stem_xp_buf[:n_xp].view(N, img, img + 2, 4)
+            self.stem_w4 = torch.zeros(c0.cout, c0.k, s8, 4, dtype=torch.bfloat16, device=self.device)
+            self.stem_dw4 = torch.zeros(c0.cout, c0.k, s8, 4, dtype=torch.float32, device=self.device)
+            g0 = self.stem_op.geom
+            self.stem_geom4 = ConvGeom(g0.stride, g0.pad_h, g0.pad_w - 1, 1)
         self.labels = torch.zeros(N, dtype=torch.int32, device=self.device)
         hs = sp.stem_hw
         self.stem_out = self._act(N, hs, hs, sp.stem.cout)
@@ -477,6 +496,12 @@ class Executor:
                 self.be.weight_tflip(src, self.wt_flat, self.wt_table, self.wt_n, self.wt_total)
             else:
                 self.be.weight_tflip(src, self.wt_flat, self.wt_table.cpu(), self.wt_n, self.wt_total)
+        self._repack_stem()
+
+    def _repack_stem(self):
+        """Packed stem weights [K][7][8][4] from the bf16 compute copy (after every update)."""
+        if self.stem_pack:
+            self.be.stem_pack_weights(self.stem_op.w, self.stem_w4)
 
     # ------------------------------------------------------------------------------------------
     # forward
@@ -532,8 +557,13 @@ class Executor:
         if train:
             be.zero_(self.stats_arena)
         st = self.stem_op
-        be.conv_fwd(self.images, st.w, self.stem_out, st.geom, stats=self.stem_stats if train else None,
-                    bn_fin=self._fin_fwd(self.stem_stats, train))
+        if self.stem_pack:
+            be.stem_pack_input(self.images, self.stem_xp)
+            be.conv_fwd(self.stem_xp, self.stem_w4, self.stem_out, self.stem_geom4,
+                        stats=self.stem_stats if train else None, bn_fin=self._fin_fwd(self.stem_stats, train))
+        else:
+            be.conv_fwd(self.images, st.w, self.stem_out, st.geom, stats=self.stem_stats if train else None,
+                        bn_fin=self._fin_fwd(self.stem_stats, train))
         if sp.maxpool:
             ph = sp.pool_hw
             pad = max((ph - 1) * 2 + 3 - sp.stem_hw, 0) // 2
@@ -675,7 +705,13 @@ class Executor:
             # still runs -- see apply_gradients
             self._tail_ev = torch.cuda.Event()
             self._tail_ev.record(self.side)
-        self._wgrad(self.images, d_stem, st.dw, st.geom)
+        if self.stem_pack:
+            if getattr(be, "wgrad_atomic_used", False):
+                be.zero_(self.stem_dw4)
+            self._wgrad(self.stem_xp, d_stem, self.stem_dw4, self.stem_geom4,
+                        post=lambda: be.stem_unpack_grad(self.stem_dw4, st.dw))
+        else:
+            self._wgrad(self.images, d_stem, st.dw, st.geom)
         self._report(0)
         if self._tail_ev is None:
             self._join()
@@ -695,14 +731,20 @@ class Executor:
             self.grad_ready(lo)
 
     # -- weight gradients on the side stream ---------------------------------------------------------
-    def _wgrad(self, x, dy, dw, geom, in_bn=None, dy_buf=None, bnb=None):
+    def _wgrad(self, x, dy, dw, geom, in_bn=None, dy_buf=None, bnb=None, post=None):
+        """Weight gradient into dw (on the side stream when enabled); post() runs right after it,
+        on the same stream (the packed stem maps its gradient back to the checkpoint layout)."""
         if self.side is None:
             self.be.conv_wgrad(x, dy, dw, geom, in_bn=in_bn, ws=self.wgrad_ws, bnb=bnb)
+            if post is not None:
+                post()
             return
         main = torch.cuda.current_stream(self.device)
         self.side.wait_stream(main)                      # x and dy are complete
         with torch.cuda.stream(self.side):
             self.be.conv_wgrad(x, dy, dw, geom, in_bn=in_bn, ws=self.wgrad_ws, bnb=bnb)
+            if post is not None:
+                post()
         if dy_buf is not None:                           # the main stream must not overwrite dy early
             ev = torch.cuda.Event()
             ev.record(self.side)
@@ -833,11 +875,12 @@ class Executor:
             wb = P.wbf16[hi:] if P.wbf16 is not None else None
             self.be.sgd_momentum(P.master[hi:], P.momentum[hi:], g[hi:], wb, self.lr_t, self.mom, self.wd,
                                  grad_scale)
-            self.refresh_dgrad_weights()
+            self.refresh_dgrad_weights(stem=False)  # (the stem's weights are not updated yet)
             self.join_grads()
             wb = P.wbf16[:hi] if P.wbf16 is not None else None
             self.be.sgd_momentum(P.master[:hi], P.momentum[:hi], g[:hi], wb, self.lr_t, self.mom, self.wd,
                                  grad_scale)
+            self._repack_stem()
             return
         self.join_grads()
         self.be.sgd_momentum(P.master, P.momentum, g, P.wbf16, self.lr_t, self.mom, self.wd, grad_scale)
@@ -851,13 +894,16 @@ class Executor:
         self.be.sgd_momentum(P.master[lo:hi], P.momentum[lo:hi], g[lo:hi], wb, self.lr_t, self.mom, self.wd,
                              grad_scale)
 
-    def refresh_dgrad_weights(self):
-        """Rebuild the flipped / channel-transposed data-gradient weights from the compute copy."""
+    def refresh_dgrad_weights(self, stem: bool = True):
+        """Rebuild the flipped / channel-transposed data-gradient weights (and the packed stem's
+        weights) from the compute copy."""
         P = self.P
         if self.wt_n:
             src = P.wbf16 if P.wbf16 is not None else P.master
             table = self.wt_table if self.is_hip else self.wt_table.cpu()
             self.be.weight_tflip(src, self.wt_flat, table, self.wt_n, self.wt_total)
+        if stem:
+            self._repack_stem()
 
     def autotune(self):
         """Run one forward + backward so the backend times and fixes its kernel configurations

@@ -23,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dataset", default="imagenet")
     ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--cprofile", type=int, default=0, help="cProfile N steps, print the top host functions")
     a = ap.parse_args()
     spec = build_spec(a.dataset, 50)
     be = HipBackend("cuda")
@@ -60,6 +61,16 @@ def main():
     t2 = time.perf_counter()
     print(f"steady: host {1e3 * (t1 - t0) / n:.2f} ms/step enqueued, wall {1e3 * (t2 - t0) / n:.2f} ms/step",
           flush=True)
+    if a.cprofile:
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(a.cprofile):
+            step()
+        pr.disable()
+        torch.cuda.synchronize()
+        pstats.Stats(pr).sort_stats("tottime").print_stats(35)
 
 
 if __name__ == "__main__":

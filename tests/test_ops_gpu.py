@@ -730,3 +730,72 @@ def test_wgrad_atomic_split_k(hip, ref, case, ns):
     hip._wgrad_full(a, ns, dw, hip.stream())
     torch.cuda.synchronize()
     assert rel(dw, dw_ref) < 1e-2
+
+
+@pytest.mark.parametrize("N,H", [(2, 16), (3, 30), (2, 224)])
+def test_packed_stem(hip, ref, N, H):
+    """Packed stem (csrc/kernels/stem.hip): the 7x7/2 conv over a 4-channel, column-padded copy of
+    the 8-channel images with tap-pair weights equals the fp32 reference of the original conv --
+    forward with BN statistics under every applicable LDS-DMA configuration, and the weight
+    gradient (every pipeline) mapped back to the [K,7,7,8] layout, padding channels exactly 0."""
+    torch.manual_seed(H)
+    K, R = 64, 7
+    P = out_size(H, R, 2, 3)
+    x = torch.zeros(N, H, H, 8)
+    x[..., :3] = torch.randn(N, H, H, 3)
+    x = bf(x)
+    w = torch.zeros(K, R, R, 8)
+    w[..., :3] = torch.randn(K, R, R, 3) * (2.0 / (R * R * 3)) ** 0.5
+    w = bf(w)
+    g8 = ConvGeom(stride=2, pad_h=3, pad_w=3)
+    g4 = ConvGeom(stride=2, pad_h=3, pad_w=2)
+    y_ref = torch.zeros(N, P, P, K)
+    st_ref = torch.zeros(2 * K)
+    ref.conv_fwd(x.float(), w.float(), y_ref, g8, stats=st_ref)
+    xd = x.cuda()
+    n_xp = N * H * (H + 2) * 4
+    buf = torch.zeros(n_xp + 64, dtype=torch.bfloat16, device="cuda")
+    xp = buf[:n_xp].view(N, H, H + 2, 4)
+    hip.stem_pack_input(xd, xp)
+    w4 = torch.zeros(K, R, 8, 4, dtype=torch.bfloat16, device="cuda")
+    hip.stem_pack_weights(w.cuda(), w4)
+    torch.cuda.synchronize()
+    # layout: interior = channels 0-3 of the images, pad columns and the tap-8 weights zero
+    assert torch.equal(xp[:, :, 1:H + 1, :].cpu(), x[..., :4])
+    assert xp[:, :, 0].abs().max().item() == 0 and xp[:, :, H + 1].abs().max().item() == 0
+    assert torch.equal(w4[:, :, :7, :].cpu(), w[..., :4]) and w4[:, :, 7].abs().max().item() == 0
+    ran = 0
+    for cfg in range(hip.L.drn_conv_glds_num_cfgs()):
+        y = torch.zeros(N, P, P, K, dtype=torch.bfloat16, device="cuda")
+        st = torch.zeros(2, 2, K, device="cuda")
+        a = hip.conv_args(xp, w4, y, g4, stats=st)
+        a.cfg = cfg
+        if hip.L.drn_conv_fwd2(ctypes.byref(a), hip.zero_page.data_ptr(), hip.stream()) != 0:
+            continue
+        torch.cuda.synchronize()
+        assert rel(y, y_ref) < 1e-2, cfg
+        s_hip = st.sum(0).view(-1).cpu()
+        assert rel(s_hip[:K], st_ref[:K]) < 2e-2 and rel(s_hip[K:], st_ref[K:]) < 2e-2, cfg
+        ran += 1
+    assert ran >= 10  # the 64-deep one-tile configurations
+    a = hip.conv_args(xp, w4, y, g4)
+    a.cfg = 100  # the packed layout exists on the LDS-DMA path only: loud refusal elsewhere
+    assert hip.L.drn_conv_fwd2(ctypes.byref(a), hip.zero_page.data_ptr(), hip.stream()) != 0
+    # weight gradient
+    dy = bf(torch.randn(N, P, P, K))
+    dw_ref = torch.zeros(K, R, R, 8)
+    ref.conv_wgrad(x.float(), dy.float(), dw_ref, g8)
+    ws = torch.zeros(max(1, hip.wgrad_ws_elems(N * P * P, K, R, 8, 4)), device="cuda")
+    old = hip.forced_wgrad_ns
+    try:
+        for ns in (2, 3, 4, 5, 6):
+            hip.forced_wgrad_ns = ns
+            dw4 = torch.zeros(K, R, 8, 4, device="cuda")
+            hip.conv_wgrad(xp, dy.cuda(), dw4, g4, ws=ws)
+            dw = torch.full((K, R, R, 8), 7.0, device="cuda")
+            hip.stem_unpack_grad(dw4, dw)
+            torch.cuda.synchronize()
+            assert rel(dw, dw_ref) < 1e-2, ns
+            assert dw[..., 4:].abs().max().item() == 0, ns
+    finally:
+        hip.forced_wgrad_ns = old
