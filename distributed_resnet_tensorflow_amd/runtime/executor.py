@@ -181,11 +181,15 @@ class Executor:
         # channel tiles: the fused prologue rewrites every input element once per output tile
         # (and again in the weight gradient), so the bottleneck expansions (128->512, 256->1024,
         # 512->2048: 4-16 tiles) spend more VALU on it than one streaming apply pass costs
-        self.mat_tiles = int(os.environ.get("DRN_BN_MAT_TILES", "100"))  # measured: 2 < 4 < 8 ~ off
+        # (ResNet-50 bs128, same box, with the 3M threshold below: tiles 8 10.25-10.31 ms, 16
+        # 10.29-10.31, 4 10.38-10.40, off 10.36-10.37 -- profiles/r2_experiments.md)
+        self.mat_tiles = int(os.environ.get("DRN_BN_MAT_TILES", "8"))
         # ... but only BN tensors of >= DRN_BN_MAT_MIN_ELEMS elements: below that a step is
         # launch-latency bound and the extra streaming launch costs more than the 3x3 consumer's
-        # in-LDS rewrite (CIFAR ResNet-50 bs 128: 2.45 ms materialised vs 2.33 ms fused)
-        self.mat_min_elems = int(os.environ.get("DRN_BN_MAT_MIN_ELEMS", str(4 << 20)))
+        # in-LDS rewrite (CIFAR ResNet-50 bs 128: 2.45 ms materialised vs 2.33 ms fused; its
+        # largest BN input is 128x32x32x16 = 2.1M). 3M: the ImageNet 7x7x512 stage (3.2M at bs128)
+        # is materialised -- its 3x3 conv and weight gradient ran 80 / 77 us with the prologue
+        self.mat_min_elems = int(os.environ.get("DRN_BN_MAT_MIN_ELEMS", "3000000"))
         self.fdt = backend.acc_dtype
         self.P = params or ParamStore(spec, self.device, keep_bf16=self.is_hip, seed=seed, dtype=self.fdt)
         self.grad_ready: Optional[Callable[[int], None]] = None

@@ -45,7 +45,7 @@ def main():
     idx = [i for i, r in enumerate(rows) if "sgd_momentum" in r["Kernel_Name"]]
     # a step may update in two launches (backward(defer_tail)): the step ends at the LAST of
     # a group of optimizer launches a few kernels apart
-    idx = [i for k, i in enumerate(idx) if k + 1 == len(idx) or idx[k + 1] - i > 4]
+    idx = [i for k, i in enumerate(idx) if k + 1 == len(idx) or idx[k + 1] - i > 16]
     step = rows[idx[-2] + 1:idx[-1] + 1]
     be = Rec()
     spec = build_spec(a.dataset, 50)

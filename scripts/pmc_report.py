@@ -24,7 +24,7 @@ def last_step(pass_dir):
         names[d] = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("drn::", "")
     order = sorted(by_disp)
     sgd = [d for d in order if "sgd_momentum" in names[d]]
-    sgd = [d for k, d in enumerate(sgd) if k + 1 == len(sgd) or sgd[k + 1] - d > 4]  # last of a group
+    sgd = [d for k, d in enumerate(sgd) if k + 1 == len(sgd) or sgd[k + 1] - d > 16]  # last of a group
     lo, hi = sgd[-2], sgd[-1]
     return [(names[d], by_disp[d]) for d in order if lo < d <= hi]
 

@@ -15,7 +15,7 @@ rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if "sgd_momentum" in r["Kernel_Name"]]
 # a step may update in two launches (backward(defer_tail)): the step ends at the LAST of
 # a group of optimizer launches a few kernels apart
-idx = [i for k, i in enumerate(idx) if k + 1 == len(idx) or idx[k + 1] - i > 4]
+idx = [i for k, i in enumerate(idx) if k + 1 == len(idx) or idx[k + 1] - i > 16]
 a, b = idx[-2] + 1, idx[-1] + 1
 step = rows[a:b]
 t0, t1 = int(step[0]["Start_Timestamp"]), int(step[-1]["End_Timestamp"])
