@@ -31,7 +31,7 @@ class Rec(RefBackend):
         M = x.shape[0] * P * Q
         self.log.append(("conv", M, K, R * S * C, x.numel() * 2 + y.numel() * 2 * (1 + (residual is not None))))
 
-    def conv_wgrad(self, x, dy, out, g, in_bn=None, relu_in=True, ws=None):
+    def conv_wgrad(self, x, dy, out, g, in_bn=None, relu_in=True, ws=None, **kw):
         K, R, S, C = out.shape
         M = dy.shape[0] * dy.shape[1] * dy.shape[2]
         self.log.append(("wgrad", M, K, R * S * C, x.numel() * 2 + dy.numel() * 2))
