@@ -98,10 +98,22 @@ __global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_wgrad_kernel(DrnCo
   const int Ktot = a.R * a.S * a.C;
   const int M = a.N * a.P * a.Q;
   const int nkt = (Ktot + BKK - 1) / BKK;
-  const int kt = blockIdx.x % nkt;
-  const int ct = blockIdx.x / nkt;
-  const int k0 = kt * BKK, c0 = ct * BCO;
+#ifndef DRN_WGRAD_NO_XCD_REMAP
+  // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs by linear id, so the
+  // (k-tile, channel-tile) blocks of one pixel split -- which all read the same pixels of x and
+  // dY -- would land on different XCDs and fetch them into 8 different L2s. Remapping the linear
+  // id keeps consecutive logical blocks (the tiles of a split) on one XCD and its L2.
+  const int ntile = gridDim.x;
+  const int lin = xcd_remap(blockIdx.x + blockIdx.y * ntile, ntile * gridDim.y);
+  const int tile = lin % ntile;
+  const int split = lin / ntile;
+#else
+  const int tile = blockIdx.x;
   const int split = blockIdx.y;
+#endif
+  const int kt = tile % nkt;
+  const int ct = tile / nkt;
+  const int k0 = kt * BKK, c0 = ct * BCO;
   const int mbeg = split * a.pix_per_split;
   const int mend = min(M, mbeg + a.pix_per_split);
 
@@ -359,10 +371,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
   const int Ktot = a.R * a.S * a.C;
   const int M = a.N * a.P * a.Q;
   const int nkt = (Ktot + BKK - 1) / BKK;
-  const int kt = blockIdx.x % nkt;
-  const int ct = blockIdx.x / nkt;
-  const int k0 = kt * BKK, c0 = ct * BCO;
+#ifndef DRN_WGRAD_NO_XCD_REMAP
+  // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs by linear id, so the
+  // (k-tile, channel-tile) blocks of one pixel split -- which all read the same pixels of x and
+  // dY -- would land on different XCDs and fetch them into 8 different L2s. Remapping the linear
+  // id keeps consecutive logical blocks (the tiles of a split) on one XCD and its L2.
+  const int ntile = gridDim.x;
+  const int lin = xcd_remap(blockIdx.x + blockIdx.y * ntile, ntile * gridDim.y);
+  const int tile = lin % ntile;
+  const int split = lin / ntile;
+#else
+  const int tile = blockIdx.x;
   const int split = blockIdx.y;
+#endif
+  const int kt = tile % nkt;
+  const int ct = tile / nkt;
+  const int k0 = kt * BKK, c0 = ct * BCO;
   const int mbeg = split * a.pix_per_split;
   const int mend = min(M, mbeg + a.pix_per_split);
 
