@@ -156,6 +156,12 @@ def main():
             for _ in range(3):
                 t_eager = min(t_eager, _time(step))
                 t_graph = min(t_graph, _time(sg.replay))
+            if world > 1:
+                # every rank takes the same decision (the slowest rank's timings)
+                tt = torch.tensor([t_eager, t_graph], dtype=torch.float64,
+                                  device="cuda" if backend == "nccl" else "cpu")
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                t_eager, t_graph = tt.tolist()
             if t_eager < t_graph:
                 run, use_graph = step, 0
     for _ in range(args.warmup):
