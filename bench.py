@@ -75,8 +75,9 @@ def main():
     spec = build_spec(args.dataset, args.resnet_size, width=args.width)
     # the P2P all-reduce (chosen by --allreduce p2p, or auto for <= 64 MB of gradients) runs the
     # data-parallel step as one HIP graph; RCCL data parallelism runs it eagerly
-    p2p = (world > 1 or force_dp) and (args.allreduce == "p2p" or
-                                       (args.allreduce == "auto" and spec.num_params() * 4 <= 64 << 20))
+    from distributed_resnet_tensorflow_amd.parallel.engine import p2p_wanted
+    p2p = (world > 1 or force_dp) and p2p_wanted(args.allreduce, spec.num_params() * 4, world,
+                                                 shard_optimizer=bool(args.shard_optimizer))
     eager_dp = (world > 1 or force_dp) and not p2p
     if (eager_dp or args.graph == 0) and args.graph != 1:
         # eager data-parallel step: its main (critical-path) stream at HIGH priority -- see
@@ -100,6 +101,7 @@ def main():
     eng = DataParallelEngine(ex, bucket_mb=args.bucket_mb, allreduce=args.allreduce, wire=args.allreduce_wire,
                              shard_optimizer=bool(args.shard_optimizer)) if (world > 1 or force_dp) else None
     if eng is not None:
+        assert (eng.p2p is not None) == p2p, "bench and engine disagree on the P2P all-reduce"
         eng.broadcast_parameters()
     # synthetic data of the benchmark shape: fixed device batch (no host input pipeline)
     be.synthetic_images(ex.images, seed=17 + rank)

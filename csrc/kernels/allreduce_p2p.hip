@@ -16,8 +16,17 @@
 //          system-scope acquire (cache invalidate), then reduces with 16-byte loads;
 //   done:   after all buckets, drn_p2p_signal(DONE); before the next step writes the gradient
 //          buffer, drn_p2p_wait(DONE) — no rank overwrites an input a peer may still be reading.
-// Every poll is bounded (DRN_P2P_SPIN_LIMIT iterations): on timeout the kernel records an error
-// code and exits, so a missing peer can never hang the GPU; the host checks the error word.
+// Every poll is bounded in TIME (P2PArgs::timeout_ms, measured on the 100 MHz s_memrealtime
+// clock): on timeout the kernel records an error code and exits, so a missing peer can never
+// hang the GPU. The error word also gates the optimizer: sgd_momentum_kernel skips the update
+// when it is set, so a step whose exchange failed leaves weights and momentum untouched; the
+// host reads a pinned copy of the word after every step (parallel/p2p.py) and aborts.
+//
+// Memory: the flag arrays and the output buffers (the two-shot all-gather reads the peers'
+// outputs) are allocated UNCACHED (hipExtMallocWithFlags(hipDeviceMallocUncached), drn_p2p_alloc)
+// and exported by IPC: a peer's system-scope store over xGMI and the owner's polling load then
+// meet in memory, with no stale copy in either XCD L2 -- the coherence a coarse-grained hipMalloc
+// buffer only gives at kernel boundaries.
 //
 // Two-shot variant for large buckets (reduce-scatter + all-gather): after READY,
 // rank r reduces only its 1/W shard of the bucket (reading that shard from all peers) into its
@@ -26,9 +35,6 @@
 // the bucket at W = 8, all 7 links busy in both phases.
 #include "drn_common.h"
 
-#ifndef DRN_P2P_SPIN_LIMIT
-#define DRN_P2P_SPIN_LIMIT (1 << 26)
-#endif
 
 namespace drn {
 
@@ -44,7 +50,8 @@ struct P2PArgs {
   const unsigned* epoch;                // device-resident step epoch (>= 1)
   int* err;                             // error word (0 = ok)
   int64_t n;                            // elements in the bucket (multiple of 4)
-  int world, rank, slot, pad_;
+  int world, rank, slot;
+  int timeout_ms;                       // bound of every device-side wait (<= 0: 60 s)
 };
 
 __device__ __forceinline__ unsigned flag_load(const unsigned* p) {
@@ -53,13 +60,15 @@ __device__ __forceinline__ unsigned flag_load(const unsigned* p) {
 
 __device__ __forceinline__ bool wait_all(const P2PArgs& a, int kind, unsigned e) {
   const unsigned* f = a.flags_local + (size_t)(a.slot * P2P_KINDS + kind) * P2P_MAX_RANKS;
-  for (int it = 0; it < DRN_P2P_SPIN_LIMIT; ++it) {
+  const unsigned long long ticks = 100000ull * (unsigned long long)(a.timeout_ms > 0 ? a.timeout_ms : 60000);
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz, independent of the shader clock
+  for (;;) {
     bool ok = true;
     for (int r = 0; r < a.world; ++r) ok = ok && flag_load(f + r) >= e;
     if (ok) return true;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) return false;
     __builtin_amdgcn_s_sleep(2);
   }
-  return false;
 }
 
 // publish this rank's epoch e for (slot, kind) to every rank (incl. itself); one thread. The
@@ -259,3 +268,16 @@ DRN_API int drn_p2p_cast(const float* x, void* y, int64_t n, hipStream_t s) {
 }
 
 DRN_API int drn_p2p_args_size() { return (int)sizeof(drn::P2PArgs); }
+
+// Zeroed UNCACHED device memory for the flag arrays / output buffers that peers access over
+// xGMI (exportable with hipIpcGetMemHandle like any device allocation); freed by drn_p2p_free.
+DRN_API int drn_p2p_alloc(void** p, size_t bytes) {
+  *p = nullptr;
+  hipError_t e = hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(*p, 0, bytes);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  return (int)e;
+}
+
+DRN_API int drn_p2p_free(void* p) { return (int)hipFree(p); }

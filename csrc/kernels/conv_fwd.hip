@@ -182,9 +182,30 @@ __device__ __forceinline__ void bn_fin_column(const DrnConvFwdArgs& a, int c0, i
 // written as whole 2*BC-byte pixel rows per wave instruction (fully coalesced). Optional
 // residual add, optional strided output map, optional per-channel sum/sumsq for the next BN,
 // or (bn_x set) the fused BN-backward reduction with ReLU-masked output.
-template <int BP, int BC, int WP, int WC, int MI, int MJ, int NT = 256, bool PF = true>
-__device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* smem, f32x4_t (&acc)[MI][MJ], int wp,
-                                              int wc, int m0, int c0, int M, const EpiPre<BP, BC, NT, PF>& e) {
+//
+// conv_epilogue_pass handles ONE channel slice [c0, c0 + BC) of the block tile: the waves that
+// own it (stage == true) write their accumulators, then every thread stores / reduces it. The
+// big-tile kernels (256 x 256) run it in NH slices because the whole fp32 tile (256 KB) does
+// not fit the 160 KB LDS; wcs = the wave's channel offset inside the slice.
+// element offset of output pixel m, channel c (-1 outside the output): epi_prefetch's map
+__device__ __forceinline__ int epi_off(const DrnConvFwdArgs& a, int m, int c, int M) {
+  if (m >= M || c >= a.K) return -1;
+  if (a.out_stride == 0) return m * a.K + c;
+  const int pq = a.P * a.Q;
+  const int n = (int)drn_fdiv((uint32_t)m, a.fd_pq);
+  const int rem = m - n * pq;
+  const int i = (int)drn_fdiv((uint32_t)rem, a.fd_q);
+  const int j = rem - i * a.Q;
+  return ((n * a.out_H + i * a.out_stride + a.out_oh) * a.out_W + j * a.out_stride + a.out_ow) * a.K + c;
+}
+
+// LAZY: output offsets computed per row here instead of held in e.off (no registers across the
+// main loop / the other slices)
+template <int BP, int BC, int WP, int MI, int MJ, int NT = 256, bool PF = true, bool LAZY = false>
+__device__ __forceinline__ void conv_epilogue_pass(const DrnConvFwdArgs& a, char* smem, f32x4_t (&acc)[MI][MJ],
+                                                   bool stage, int wp, int wcs, int m0, int c0, int M,
+                                                   const EpiPre<BP, BC, NT, PF>& e) {
+  static_assert(!(LAZY && PF), "lazy offsets: no prefetched operands");
   using E = EpiPre<BP, BC, NT, PF>;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -193,13 +214,15 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
   constexpr int RPI = E::RPI;
   constexpr int SWM = CF >= 8 ? 7 : CF - 1;  // swizzle mask stays inside a staged row
   float* tile = reinterpret_cast<float*>(smem);
+  if (stage) {
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const int cf = (wc * WC + i * 16) / 4 + (lane >> 4);  // fp32 chunk of these 4 channels
+    for (int i = 0; i < MI; ++i) {
+      const int cf = (wcs + i * 16) / 4 + (lane >> 4);  // fp32 chunk of these 4 channels
 #pragma unroll
-    for (int j = 0; j < MJ; ++j) {
-      const int row = wp * WP + j * 16 + (lane & 15);
-      *reinterpret_cast<f32x4_t*>(tile + row * BC + ((cf ^ (row & SWM)) * 4)) = acc[i][j];
+      for (int j = 0; j < MJ; ++j) {
+        const int row = wp * WP + j * 16 + (lane & 15);
+        *reinterpret_cast<f32x4_t*>(tile + row * BC + ((cf ^ (row & SWM)) * 4)) = acc[i][j];
+      }
     }
   }
   __syncthreads();
@@ -222,12 +245,12 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
       bis[j] = a.bn_invstd[c + j];
     }
   }
-#pragma unroll
+#pragma unroll(LAZY ? 2 : E::IT)
   for (int it = 0; it < E::IT; ++it) {
     const int row = it * RPI + tid / CHR;
     const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(tile + row * BC + (((2 * ch) ^ (row & SWM)) * 4));
     const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(tile + row * BC + (((2 * ch + 1) ^ (row & SWM)) * 4));
-    const int off = e.off[it];
+    const int off = LAZY ? epi_off(a, m0 + row, c, M) : e.off[it];
     if (off >= 0) {
       float f[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       if (has_res) {
@@ -310,8 +333,32 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
       const int rep = a.stats_rep > 1 ? a.stats_rep : 1;
       if (c0 + cl < a.K) atomicAdd(a.stats + ((size_t)(blockIdx.x % rep) * 2 + which) * a.K + c0 + cl, s);
     }
-    if (a.fin_cnt != nullptr) bn_fin_column<BP, BC, NT>(a, c0, M, reinterpret_cast<int*>(smem));
   }
+}
+
+template <int BP, int BC, int WP, int WC, int MI, int MJ, int NT = 256, bool PF = true>
+__device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* smem, f32x4_t (&acc)[MI][MJ], int wp,
+                                              int wc, int m0, int c0, int M, const EpiPre<BP, BC, NT, PF>& e) {
+  conv_epilogue_pass<BP, BC, WP, MI, MJ, NT, PF>(a, smem, acc, true, wp, wc * WC, m0, c0, M, e);
+  if (a.stats != nullptr && a.fin_cnt != nullptr) bn_fin_column<BP, BC, NT>(a, c0, M, reinterpret_cast<int*>(smem));
+}
+
+// NH channel slices of BC / NH (each wave's WC channels lie inside one slice); no prefetched
+// epilogue operands (the big tiles spend their registers on accumulators)
+template <int BP, int BC, int WP, int WC, int MI, int MJ, int NT, int NH>
+__device__ __forceinline__ void conv_epilogue_sliced(const DrnConvFwdArgs& a, char* smem, f32x4_t (&acc)[MI][MJ],
+                                                     int wp, int wc, int m0, int c0, int M) {
+  constexpr int BCH = BC / NH;
+  static_assert(BC % NH == 0 && BCH % WC == 0, "a wave's channels must lie inside one slice");
+#pragma unroll 1
+  for (int h = 0; h < NH; ++h) {
+    if (h > 0) __syncthreads();  // the previous slice's LDS reads / reductions are done
+    EpiPre<BP, BCH, NT, false> e;  // unused (LAZY offsets)
+    const int wcs = wc * WC - h * BCH;
+    conv_epilogue_pass<BP, BCH, WP, MI, MJ, NT, false, true>(a, smem, acc, wcs >= 0 && wcs < BCH, wp, wcs, m0,
+                                                             c0 + h * BCH, M, e);
+  }
+  if (a.stats != nullptr && a.fin_cnt != nullptr) bn_fin_column<BP, BC, NT>(a, c0, M, reinterpret_cast<int*>(smem));
 }
 
 template <int BP, int BC, int BK, int WP, int WC, bool PRO, bool DIL2>
@@ -609,7 +656,7 @@ __device__ __forceinline__ int glds_swz(int row) {
 // The coefficients come from the BN statistics replicas in the prologue (consumer-side
 // finalize; the first workgroup of the publishing launch writes dgamma / dbeta).
 template <int BP, int BC, int WAVES_P, int NS, int NW = 4, bool PF = true, int BK = 64, bool PRO = false,
-          bool SROW = false, bool BNB = false>
+          bool SROW = false, bool BNB = false, int NH = 1>
 __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a, const void* __restrict__ zero) {
   static_assert(BK == 64 || BK == 32, "k per stage");
   static_assert(!SROW || BK == 64, "row-staged narrow convs: 64-deep stages");
@@ -628,6 +675,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   static_assert(WAVES_P * WAVES_C == NW && MI >= 1 && MJ >= 1, "wave layout");
   static_assert(GA * RPG * NW == BC && GB * RPG * NW == BP, "rows must split evenly over the waves");
   static_assert(NS >= 2 && G * (D > 1 ? D - 1 : 1) < 64, "pipeline depth");
+  static_assert(NH == 1 || (!PF && !SROW && !BNB), "sliced epilogue: big-tile plain / PRO kernels only");
 
   extern __shared__ __attribute__((aligned(1024))) char smem[];
 
@@ -768,8 +816,9 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   static_assert((RPG * NW) % 16 == 0, "piece stride must preserve the swizzle bits");
   const int lcb = lpc ^ glds_swz<BK>(RPG * wave + lrow);
   int xr = 0, xs = 0, xci = 0;  // tap / channel offset of the stage being transformed
-  EpiPre<BP, BC, NT, PF> epre;
-  epi_prefetch<BP, BC, NT, PF>(a, m0, c0, M, epre);  // residual / BN inputs in flight during the main loop
+  EpiPre<BP, BC / NH, NT, PF> epre;
+  if constexpr (NH == 1)
+    epi_prefetch<BP, BC, NT, PF>(a, m0, c0, M, epre);  // residual / BN inputs in flight during the main loop
 #pragma unroll
   for (int s = 0; s < D; ++s)
     if (s < T) issue(s);
@@ -886,11 +935,13 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
       for (int i = 0; i < MI; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(st + aoff[i] + slot);
 #pragma unroll
       for (int j = 0; j < MJ; ++j) bfr[j] = *reinterpret_cast<const bf16x8_t*>(st + boffl[j] + slot);
+      if constexpr (NW == 8) __builtin_amdgcn_s_setprio(1);  // keeps the MFMA cluster together (guide T5)
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < MJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if constexpr (NW == 8) __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("" ::: "memory");
   }
@@ -899,8 +950,9 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   unsigned long long t_loop = 0;
   if (trace != nullptr) t_loop = drn_realtime();
 #endif
-  // (the launcher sizes the dynamic LDS for max(NS * STAGE, BP * BC * 4))
-  conv_epilogue<BP, BC, WP, WC, MI, MJ, NT, PF>(a, smem, acc, wp, wc, m0, c0, M, epre);
+  // (the launcher sizes the dynamic LDS for max(NS * STAGE, BP * BC * 4 / NH))
+  if constexpr (NH == 1) conv_epilogue<BP, BC, WP, WC, MI, MJ, NT, PF>(a, smem, acc, wp, wc, m0, c0, M, epre);
+  else conv_epilogue_sliced<BP, BC, WP, WC, MI, MJ, NT, NH>(a, smem, acc, wp, wc, m0, c0, M);
 #ifdef DRN_CONV_TRACE
   if (trace != nullptr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -928,16 +980,17 @@ static int cfin_max_blocks() {
   return v;
 }
 
-template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF, int BK, bool PRO, bool SROW = false, bool BNB = false>
+template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF, int BK, bool PRO, bool SROW = false, bool BNB = false,
+          int NH = 1>
 static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
   const int T = a->C == 4 ? (a->R + 1) / 2 : a->C == 8 || a->C == 16 ? a->R : (a->R * a->S * a->C) / BK;  // k-stages
                                                           // (SROW: filter rows; packed stem: row pairs)
   const int LDS0 = (T < NS ? T : NS) * (BC + BP * (BNB ? 2 : 1)) * BK * 2;  // stage slots actually used
   const int lds_main = LDS0 + (PRO ? 8 * a->C : 0) + (BNB ? 12 * a->C : 0);  // + fused-BN parameters
-  const int LDS = lds_main > BP * BC * 4 ? lds_main : BP * BC * 4;  // epilogue staging tile
+  const int LDS = lds_main > BP * BC * 4 / NH ? lds_main : BP * BC * 4 / NH;  // epilogue staging slice
   if (LDS > 160 * 1024) return (int)hipErrorInvalidValue;
   static bool attr_set = false;
-  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS, NW, PF, BK, PRO, SROW, BNB>;
+  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS, NW, PF, BK, PRO, SROW, BNB, NH>;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
@@ -962,9 +1015,24 @@ static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t 
   return (int)hipGetLastError();
 }
 
+template <int BP, int BC, int WAVES_P, int NS, int NW, int BK>
+static int launch_conv_glds_nh1(DrnConvFwdArgs* a, const void* zero, hipStream_t stream);
+
 // epilogue operands (residual / BN-backward input) are prefetched only when present
-template <int BP, int BC, int WAVES_P, int NS, int NW = 4, int BK = 64>
+template <int BP, int BC, int WAVES_P, int NS, int NW = 4, int BK = 64, int NH = 1>
 static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
+  if constexpr (NH > 1) {  // big tiles: plain / fused-BN-prologue input, sliced epilogue, no prefetch
+    if (a->C == 4 || a->C == 8 || a->C == 16 || a->C % BK || a->bnb_x != nullptr) return (int)hipErrorInvalidValue;
+    if (a->in_scale != nullptr)
+      return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, true, false, false, NH>(a, zero, stream);
+    return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false, false, false, NH>(a, zero, stream);
+  } else {
+    return launch_conv_glds_nh1<BP, BC, WAVES_P, NS, NW, BK>(a, zero, stream);
+  }
+}
+
+template <int BP, int BC, int WAVES_P, int NS, int NW, int BK>
+static int launch_conv_glds_nh1(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
   const bool pf = a->residual != nullptr || a->bn_x != nullptr;
   if (a->C == 4 || a->C == 8 || a->C == 16) {  // row-staged narrow conv (the stem, the CIFAR first stage)
     if constexpr (BK == 64) {
@@ -993,39 +1061,48 @@ static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t str
 }
 
 // Tile configurations of the LDS-DMA kernel (index = DRN conv config id, also used by the
-// host-side autotuner): {BP, BC, WAVES_P, NS}.
-#define DRN_GLDS_CONFIGS(X)  \
-  X(0, 128, 128, 2, 2, 4)    \
-  X(1, 128, 128, 2, 3, 4)    \
-  X(2, 128, 128, 2, 4, 4)    \
-  X(3, 256, 64, 4, 2, 4)     \
-  X(4, 256, 64, 4, 3, 4)     \
-  X(5, 128, 64, 2, 3, 4)     \
-  X(6, 64, 128, 1, 3, 4)     \
-  X(7, 64, 64, 2, 4, 4)      \
-  X(8, 256, 128, 4, 2, 8)    \
-  X(9, 256, 128, 4, 3, 8)    \
-  X(10, 128, 256, 2, 2, 8)   \
-  X(11, 128, 256, 2, 3, 8)   \
-  X(12, 128, 64, 2, 2, 4)    \
-  X(13, 64, 128, 1, 2, 4)    \
-  X(14, 64, 64, 2, 2, 4)     \
-  X(15, 64, 256, 1, 2, 4)    \
-  X(16, 32, 128, 1, 2, 4)    \
-  X(17, 128, 128, 2, 4, 4, 32) \
-  X(18, 64, 128, 1, 4, 4, 32)  \
-  X(19, 128, 64, 2, 4, 4, 32)  \
-  X(20, 128, 128, 2, 3, 4, 32) \
-  X(21, 64, 128, 1, 3, 4, 32)  \
-  X(22, 256, 64, 4, 4, 4, 32)  \
-  X(23, 256, 32, 4, 2, 4)      \
-  X(24, 128, 32, 4, 3, 4)
+// host-side autotuner): {BP, BC, WAVES_P, NS, NW, BK, NH}. 25-30 are the 8-wave big tiles with
+// 32-deep stages and 3-4 stages in flight (one workgroup per CU, ~96 KB of LDS-DMA in flight):
+// a 128 x 128 tile needs 64 B per MFMA cycle from L2 -- the per-CU L2 read rate -- so it can
+// never keep the matrix pipe busy; 256 x 256 needs half that, 256 x 128 three quarters.
+#define DRN_GLDS_CONFIGS(X)      \
+  X(0, 128, 128, 2, 2, 4, 64, 1)  \
+  X(1, 128, 128, 2, 3, 4, 64, 1)  \
+  X(2, 128, 128, 2, 4, 4, 64, 1)  \
+  X(3, 256, 64, 4, 2, 4, 64, 1)   \
+  X(4, 256, 64, 4, 3, 4, 64, 1)   \
+  X(5, 128, 64, 2, 3, 4, 64, 1)   \
+  X(6, 64, 128, 1, 3, 4, 64, 1)   \
+  X(7, 64, 64, 2, 4, 4, 64, 1)    \
+  X(8, 256, 128, 4, 2, 8, 64, 1)  \
+  X(9, 256, 128, 4, 3, 8, 64, 1)  \
+  X(10, 128, 256, 2, 2, 8, 64, 1) \
+  X(11, 128, 256, 2, 3, 8, 64, 1) \
+  X(12, 128, 64, 2, 2, 4, 64, 1)  \
+  X(13, 64, 128, 1, 2, 4, 64, 1)  \
+  X(14, 64, 64, 2, 2, 4, 64, 1)   \
+  X(15, 64, 256, 1, 2, 4, 64, 1)  \
+  X(16, 32, 128, 1, 2, 4, 64, 1)  \
+  X(17, 128, 128, 2, 4, 4, 32, 1) \
+  X(18, 64, 128, 1, 4, 4, 32, 1)  \
+  X(19, 128, 64, 2, 4, 4, 32, 1)  \
+  X(20, 128, 128, 2, 3, 4, 32, 1) \
+  X(21, 64, 128, 1, 3, 4, 32, 1)  \
+  X(22, 256, 64, 4, 4, 4, 32, 1)  \
+  X(23, 256, 32, 4, 2, 4, 64, 1)  \
+  X(24, 128, 32, 4, 3, 4, 64, 1)  \
+  X(25, 256, 256, 4, 4, 8, 32, 2) \
+  X(26, 256, 256, 4, 2, 8, 64, 2) \
+  X(27, 256, 128, 4, 5, 8, 32, 1) \
+  X(28, 128, 256, 2, 5, 8, 32, 1) \
+  X(29, 256, 256, 2, 4, 8, 32, 2) \
+  X(30, 256, 128, 2, 4, 8, 32, 1)
 
 static int launch_glds_cfg(int cfg, DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
   switch (cfg) {
-#define DRN_X(id, bp, bc, wpv, ns, nw, ...) \
-  case id:                                  \
-    return launch_conv_glds<bp, bc, wpv, ns, nw __VA_OPT__(, ) __VA_ARGS__>(a, zero, s);
+#define DRN_X(id, bp, bc, wpv, ns, nw, bk, nh) \
+  case id:                                     \
+    return launch_conv_glds<bp, bc, wpv, ns, nw, bk, nh>(a, zero, s);
     DRN_GLDS_CONFIGS(DRN_X)
 #undef DRN_X
     default:
@@ -1035,8 +1112,8 @@ static int launch_glds_cfg(int cfg, DrnConvFwdArgs* a, const void* zero, hipStre
 
 static int glds_cfg_bp(int cfg) {
   switch (cfg) {
-#define DRN_X(id, bp, bc, wpv, ns, nw, ...) \
-  case id:                                  \
+#define DRN_X(id, bp, bc, wpv, ns, nw, bk, nh) \
+  case id:                                     \
     return bp;
     DRN_GLDS_CONFIGS(DRN_X)
 #undef DRN_X
@@ -1098,7 +1175,7 @@ DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s);
 DRN_API int drn_conv_mt(int cfg, DrnConvFwdArgs* a, const void* zero, hipStream_t s);
 DRN_API int drn_conv_mt_num_cfgs();
 DRN_API int drn_conv_mt_ok(const DrnConvFwdArgs* a);
-#define DRN_GLDS_NCFG 25
+#define DRN_GLDS_NCFG 31
 
 // Whether the LDS-DMA kernel family supports this convolution.
 DRN_API int drn_conv_glds_ok(const DrnConvFwdArgs* a) {

@@ -16,7 +16,9 @@ namespace drn {
 __global__ __launch_bounds__(256) void sgd_momentum_kernel(float* __restrict__ w, float* __restrict__ m,
                                                            const float* __restrict__ g, bf16_t* __restrict__ wb,
                                                            int64_t n4, const float* __restrict__ lr_ptr, float mu,
-                                                           float wd, float grad_scale) {
+                                                           float wd, float grad_scale, const int* __restrict__ skip) {
+  // skip: the step's gradient exchange failed (P2P error word): apply no update at all
+  if (skip != nullptr && *skip != 0) return;
   const float lr = *lr_ptr;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
     float4 wv = reinterpret_cast<float4*>(w)[i];
@@ -129,11 +131,12 @@ static inline int grid_for(int64_t n) {
 
 }  // namespace drn
 
+// skip (nullable device int): when *skip != 0 at run time the launch changes nothing
 DRN_API int drn_sgd_momentum(float* w, float* m, const float* g, void* w_bf16, int64_t n, const float* lr_ptr,
-                             float momentum, float wd, float grad_scale, hipStream_t s) {
+                             float momentum, float wd, float grad_scale, const int* skip, hipStream_t s) {
   if (n % 4) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(drn::sgd_momentum_kernel, dim3(drn::grid_for(n / 4)), dim3(256), 0, s, w, m, g,
-                     (bf16_t*)w_bf16, n / 4, lr_ptr, momentum, wd, grad_scale);
+                     (bf16_t*)w_bf16, n / 4, lr_ptr, momentum, wd, grad_scale, skip);
   return (int)hipGetLastError();
 }
 

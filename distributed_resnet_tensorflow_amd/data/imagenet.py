@@ -277,29 +277,49 @@ class ImagenetLoader:
         label = int(ex.get("image/class/label", [-1])[0])
         return img, label
 
+    def _batches(self):
+        """(futures of one batch's decodes, epoch, cursor-after), with the NEXT batch's decodes
+        already submitted before the current one is handed on: the pool never idles on the
+        slowest image of a batch (two batches in flight)."""
+        inflight, batch = [], []
+        for s, r, epoch, cursor in self._positions():
+            batch.append((s, r))
+            if len(batch) < self.bs:
+                continue
+            inflight.append(([self.pool.submit(self._decode, pos) for pos in batch], epoch, cursor))
+            batch = []
+            if len(inflight) > 1:
+                yield inflight.pop(0)
+        yield from inflight
+
+    def _host(self, n: int, dtype):
+        """A fresh host buffer (page-locked with pin=True, so its async H2D copy never stages
+        through pageable memory): (object handed on, numpy view). Pinned int32 buffers are
+        int32 tensors; other pinned dtypes are raw uint8 tensors."""
+        if not self.pin:
+            a = np.empty(n, dtype=dtype)
+            return a, a
+        import torch
+        if np.dtype(dtype) == np.int32:
+            t = torch.empty(n, dtype=torch.int32, pin_memory=True)
+            return t, t.numpy()
+        t = torch.empty(n * np.dtype(dtype).itemsize, dtype=torch.uint8, pin_memory=True)
+        return t, t.numpy().view(dtype)
+
     def _run(self):
         b = self.batch_index
-        batch = []
         try:
             if self.pin and self.pin_device is not None:
                 import torch
                 torch.cuda.set_device(self.pin_device)
-            for s, r, epoch, cursor in self._positions():
-                batch.append((s, r))
-                if len(batch) < self.bs:
-                    continue
-                decoded = list(self.pool.map(self._decode, batch))
-                batch = []
+            for futs, epoch, cursor in self._batches():
+                decoded = [f.result() for f in futs]
                 rng = np.random.default_rng([self.seed, self.rank, 99, b])
                 total = sum(d[0].size for d in decoded)
-                if self.pin:
-                    import torch
-                    packed = torch.empty(total, dtype=torch.uint8, pin_memory=True)
-                    flat = packed.numpy()
-                else:
-                    packed = flat = np.empty(total, dtype=np.uint8)
-                desc = np.zeros(self.bs, dtype=IMG_DESC)
-                labels = np.empty(self.bs, dtype=np.int32)
+                packed, flat = self._host(total, np.uint8)
+                desc_h, desc = self._host(self.bs, IMG_DESC)
+                labels_h, labels = self._host(self.bs, np.int32)
+                desc[...] = np.zeros((), dtype=IMG_DESC)
                 off = 0
                 for i, (img, lab) in enumerate(decoded):
                     h, w = img.shape[:2]
@@ -309,7 +329,9 @@ class ImagenetLoader:
                     labels[i] = lab
                     off += img.size
                 b += 1
-                item = (packed, desc, labels, {"data_epoch": epoch, "data_cursor": cursor, "data_batch": b})
+                # pin=True: the page-locked tensors themselves (desc as raw IMG_DESC bytes), so the
+                # caching host allocator tracks their async copies
+                item = (packed, desc_h, labels_h, {"data_epoch": epoch, "data_cursor": cursor, "data_batch": b})
                 while not self._stop.is_set():
                     try:
                         self.q.put(item, timeout=0.1)

@@ -108,7 +108,7 @@ _SIGS = {
     "drn_colsum": ([c_p, c_int, c_int, c_p, c_f, c_int, c_p], c_int),
     "drn_maxpool_fwd": ([c_p, c_p, c_p] + [c_int] * 10 + [c_p, c_int, c_p], c_int),
     "drn_maxpool_bwd": ([c_p, c_p, c_p] + [c_int] * 10 + [c_p], c_int),
-    "drn_sgd_momentum": ([c_p, c_p, c_p, c_p, c_i64, c_p, c_f, c_f, c_f, c_p], c_int),
+    "drn_sgd_momentum": ([c_p, c_p, c_p, c_p, c_i64, c_p, c_f, c_f, c_f, c_p, c_p], c_int),
     "drn_cast_bf16": ([c_p, c_p, c_i64, c_p], c_int),
     "drn_stem_pack_input": ([c_p, c_p, c_int, c_int, c_p], c_int),
     "drn_stem_pack_weights": ([c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p], c_int),
@@ -123,6 +123,8 @@ _SIGS = {
     "drn_p2p_step": ([c_p, c_p, c_p], c_int),
     "drn_p2p_cast": ([c_p, c_p, c_i64, c_p], c_int),
     "drn_p2p_args_size": ([], c_int),
+    "drn_p2p_alloc": ([ctypes.POINTER(c_p), ctypes.c_size_t], c_int),
+    "drn_p2p_free": ([c_p], c_int),
     "drn_bn_fin_size": ([], c_int),
     "drn_conv_args_size": ([], c_int),
     "drn_wgrad_args_size": ([], c_int),
@@ -170,8 +172,28 @@ def lib():
                          ("drn_wgrad_args_size", DrnConvWgradArgs)):
             if getattr(h, name)() != ctypes.sizeof(st):
                 raise KernelLibraryError(f"{st.__name__} layout mismatch between Python and {LIB_PATH.name}")
+        _check_stamp(h)
         _LIB = h
         return _LIB
+
+
+def _check_stamp(h) -> None:
+    """Refuse a library built from other kernel sources than the tree's (source hash compiled in by
+    ops.build); skipped when the sources are absent (an installed library) or for an explicit
+    A/B library (DRN_KERNEL_LIB)."""
+    from . import build as _build
+    if os.environ.get("DRN_KERNEL_LIB") or not any(_build.KERNELS.glob("*.hip")):
+        return
+    if not hasattr(h, "drn_src_hash"):
+        raise KernelLibraryError(f"{LIB_PATH} has no source stamp: rebuild it (python -m "
+                                 "distributed_resnet_tensorflow_amd.ops.build)")
+    h.drn_src_hash.restype = ctypes.c_char_p
+    h.drn_src_hash.argtypes = []
+    built = h.drn_src_hash().decode()
+    want = _build.source_hash()
+    if built != want:
+        raise KernelLibraryError(f"{LIB_PATH} was built from different kernel sources (stamp {built[:12]}, tree "
+                                 f"{want[:12]}): rebuild it (python -m distributed_resnet_tensorflow_amd.ops.build)")
 
 
 def check(rc: int, what: str) -> None:

@@ -665,10 +665,12 @@ class HipBackend(_Common):
                                           pad_h, pad_w, self.stream()), "drn_maxpool_bwd")
 
     # -- optimizer / weights ------------------------------------------------------------------------
-    def sgd_momentum(self, w, m, g, wb, lr_t, momentum, wd, grad_scale):
+    def sgd_momentum(self, w, m, g, wb, lr_t, momentum, wd, grad_scale, skip=None):
+        """Fused SGD-momentum; skip = optional device int32 word: the launch changes nothing when
+        it holds a non-zero value at run time (a failed P2P gradient exchange)."""
         _lib.check(self.L.drn_sgd_momentum(w.data_ptr(), m.data_ptr(), g.data_ptr(), _ptr(wb), w.numel(),
                                            lr_t.data_ptr(), float(momentum), float(wd), float(grad_scale),
-                                           self.stream()), "drn_sgd_momentum")
+                                           _ptr(skip), self.stream()), "drn_sgd_momentum")
 
     def cast_bf16(self, x, y):
         _lib.check(self.L.drn_cast_bf16(x.data_ptr(), y.data_ptr(), x.numel(), self.stream()), "drn_cast_bf16")
@@ -1004,7 +1006,9 @@ class RefBackend(_Common):
                 acc[:, r:r + (P - 1) * stride + 1:stride, s:s + (Q - 1) * stride + 1:stride, :] += m
         dx.copy_(acc[:, pad_h:pad_h + H, pad_w:pad_w + W, :])
 
-    def sgd_momentum(self, w, m, g, wb, lr_t, momentum, wd, grad_scale):
+    def sgd_momentum(self, w, m, g, wb, lr_t, momentum, wd, grad_scale, skip=None):
+        if skip is not None and int(skip.reshape(-1)[0]) != 0:
+            return
         lr = float(lr_t.reshape(-1)[0])
         gg = g * grad_scale + wd * w
         m.mul_(momentum).add_(gg)

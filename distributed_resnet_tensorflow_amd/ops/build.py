@@ -44,6 +44,34 @@ def sources() -> list[Path]:
     return sorted(KERNELS.glob("*.hip"))
 
 
+def source_hash(kernels: Path = KERNELS, include: Path = INCLUDE) -> str:
+    """sha256 over every kernel source and shared header (relative name + bytes). Compiled into
+    the library (drn_src_hash) and checked by ops._lib.lib(), so a library built from other
+    sources is refused whatever the file times say."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(kernels.glob("*.hip")) + sorted(include.glob("*.h")):
+        h.update(f.parent.name.encode() + b"/" + f.name.encode() + b"\0")
+        h.update(f.read_bytes())
+    return h.hexdigest()
+
+
+def _stamp_object() -> Path:
+    """A one-function translation unit returning source_hash(), rebuilt when the hash changes."""
+    gen = OBJ_DIR / "drn_src_stamp.cc"
+    text = ('extern "C" __attribute__((visibility("default"))) const char* drn_src_hash() '
+            f'{{ return "{source_hash()}"; }}\n')
+    if not gen.exists() or gen.read_text() != text:
+        gen.write_text(text)
+    obj = gen.with_suffix(".o")
+    if not obj.exists() or obj.stat().st_mtime < gen.stat().st_mtime:
+        cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
+        res = subprocess.run([cxx, "-O2", "-fPIC", "-c", str(gen), "-o", str(obj)], capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"source stamp build failed:\n{res.stderr[-2000:]}")
+    return obj
+
+
 def _headers_mtime() -> float:
     hs = list(INCLUDE.glob("*.h"))
     return max((h.stat().st_mtime for h in hs), default=0.0)
@@ -114,6 +142,7 @@ def build(force: bool = False, verbose: bool = True, extra: list[str] | None = N
     jobs = min(len(srcs), max(1, min(8, (os.cpu_count() or 4))))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, extra), srcs))
+    objs.append(_stamp_object())
     newest = max(o.stat().st_mtime for o in objs)
     if LIB_PATH.exists() and LIB_PATH.stat().st_mtime >= newest and not force:
         if verbose:

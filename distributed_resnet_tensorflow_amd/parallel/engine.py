@@ -64,6 +64,22 @@ def use_priority_main_stream():
     return s
 
 
+def p2p_wanted(allreduce: str, grad_bytes: int, world: int, mode: str = "sync", shard_optimizer: bool = False,
+               p2p_max_mb: float = 64.0) -> bool:
+    """The one decision of whether the data-parallel step uses the P2P all-reduce (shared by the
+    engine and bench.py). `p2p` forces it (the engine then validates the combination); `auto`
+    picks it only for a small whole gradient (latency-bound CIFAR buckets) on ONE node
+    (LOCAL_WORLD_SIZE == WORLD_SIZE: HIP IPC cannot map a peer on another host), synchronous
+    mode and no optimizer sharding (which needs reduce-scatter / all-gather collectives)."""
+    if allreduce == "p2p":
+        return True
+    if allreduce != "auto" or world > 8 or mode != "sync" or shard_optimizer:
+        return False
+    if int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) != world:
+        return False
+    return grad_bytes <= p2p_max_mb * (1 << 20)
+
+
 class DataParallelEngine:
     def __init__(self, executor, bucket_mb: float = 25.0, mode: str = "sync", group=None,
                  allreduce: str = "rccl", p2p_max_mb: float = 64.0, first_bucket_mb: float = 2.0,
@@ -83,8 +99,7 @@ class DataParallelEngine:
         self.wire = (wire or os.environ.get("DRN_ALLREDUCE_WIRE", "fp32")).lower()
         if self.wire not in ("fp32", "bf16"):
             raise ValueError(f"all-reduce wire type must be fp32 or bf16, got {self.wire!r}")
-        total_mb = self.P.total * 4 / (1 << 20)
-        want = allreduce == "p2p" or (allreduce == "auto" and total_mb <= p2p_max_mb)
+        want = p2p_wanted(allreduce, self.P.total * 4, self.world, mode, shard_optimizer, p2p_max_mb)
         if want and self.P.grad.is_cuda and mode == "sync" and self.world <= 8 \
                 and dist.get_backend(group) in ("nccl", "gloo"):
             from .p2p import P2PAllReduce
@@ -261,7 +276,9 @@ class DataParallelEngine:
         -- ZeRO-1 -- the update of this rank's shards followed by the all-gather of the compute
         weights and the refresh of the data-gradient weights."""
         if not self.zero1:
-            self.ex.apply_gradients(grad_scale=grad_scale, grad=grad)
+            # P2P: the optimizer reads the exchange's error word and skips a failed step's update
+            self.ex.apply_gradients(grad_scale=grad_scale, grad=grad,
+                                    skip=self.p2p.err if self.p2p is not None else None)
             return
         for lo, hi in self.buckets:
             s0, s1 = self._shard(lo, hi)
@@ -293,6 +310,31 @@ class DataParallelEngine:
         t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
         dist.broadcast(t, src=dist.get_global_rank(self.group, 0) if self.group is not None else 0, group=self.group)
         return bool(t.item())
+
+    # -- whole-step graph replays (P2P data parallelism) ---------------------------------------------
+    def replay_begin(self):
+        """Host bookkeeping that the captured step no longer runs: the step counter and the
+        collective watchdog's arm (a replayed step re-arms it like an eager one)."""
+        self._step_no += 1
+        if self.watchdog is not None:
+            self.watchdog.arm(self._step_no)
+
+    def replay_end(self):
+        if self.watchdog is not None:
+            ev = torch.cuda.Event() if self.cuda else None
+            if ev is not None:
+                ev.record()
+            self.watchdog.done(ev)
+
+    def poll_errors(self):
+        """Non-blocking check of the P2P error word of completed steps (raises on failure)."""
+        if self.p2p is not None:
+            self.p2p.poll()
+
+    def check_errors(self):
+        """Synchronous check (before a checkpoint is written)."""
+        if self.p2p is not None:
+            self.p2p.check()
 
     def stats(self) -> dict:
         """Timing of the last completed step (synchronizes on its events)."""

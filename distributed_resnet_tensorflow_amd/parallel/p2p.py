@@ -17,6 +17,17 @@ bytes every GPU pulls over xGMI: each bucket is first cast to a bf16 shadow buff
 mapped) on the compute stream and the peers read the shadows, accumulating in fp32 (the same
 trade as Horovod's fp16 gradient compression).
 
+Failure handling: every device-side wait is bounded in time (DRN_P2P_TIMEOUT_MS, default
+60000). A timed-out wait sets the error word and returns; the optimizer launch reads the same
+word and applies NO update (weights and momentum stay bitwise unchanged), and end_step() queues
+a copy of the word into pinned host memory -- inside a captured HIP graph too -- which the
+training session reads after every step without a device sync (poll()) and turns into an
+exception; a checkpoint is only written after a synchronous check().
+
+Memory: the flag arrays and the fp32 output buffers (read by the peers in the two-shot
+all-gather) are UNCACHED device allocations (drn_p2p_alloc), exported by IPC: peer stores over
+xGMI and local polling loads meet in memory, with no stale XCD-L2 copy on either side.
+
 Limits: one node, <= 8 ranks, fp32 buckets whose element count is a multiple of 4.
 """
 from __future__ import annotations
@@ -59,7 +70,7 @@ class P2PArgs(ctypes.Structure):
         ("epoch", ctypes.c_void_p),
         ("err", ctypes.c_void_p),
         ("n", ctypes.c_int64),
-        ("world", ctypes.c_int), ("rank", ctypes.c_int), ("slot", ctypes.c_int), ("pad_", ctypes.c_int),
+        ("world", ctypes.c_int), ("rank", ctypes.c_int), ("slot", ctypes.c_int), ("timeout_ms", ctypes.c_int),
     ]
 
 
@@ -94,6 +105,30 @@ def _export(t: torch.Tensor):
     return handle.to_bytes(), t.data_ptr() - base.value
 
 
+class _DeviceBuffer:
+    """An uncached device allocation exposed to torch through __cuda_array_interface__ (the
+    tensor does not own it: keep this object alive, release() frees it)."""
+
+    def __init__(self, L, numel: int, dtype: torch.dtype, device: torch.device):
+        self.L = L
+        esize = torch.empty((), dtype=dtype).element_size()
+        p = ctypes.c_void_p()
+        _lib.check(L.drn_p2p_alloc(ctypes.byref(p), max(1, numel) * esize), "drn_p2p_alloc (uncached)")
+        self.ptr = p.value
+        typestr = {torch.float32: "<f4", torch.int32: "<i4"}[dtype]
+        self.__cuda_array_interface__ = {"shape": (numel,), "typestr": typestr, "data": (self.ptr, False),
+                                         "version": 2, "strides": None}
+        self.tensor = torch.as_tensor(self, device=device)
+        if self.tensor.data_ptr() != self.ptr or self.tensor.device.type != "cuda":
+            raise RuntimeError("uncached P2P buffer could not be wrapped as a device tensor")
+
+    def release(self):
+        if self.ptr is not None:
+            self.tensor = None
+            self.L.drn_p2p_free(ctypes.c_void_p(self.ptr))
+            self.ptr = None
+
+
 class P2PAllReduce:
     """Maps every rank's `grad` (and flag words) and reduces buckets of it into `out`."""
 
@@ -115,10 +150,19 @@ class P2PAllReduce:
         self.wire = (wire or os.environ.get("DRN_P2P_WIRE", "fp32")).lower()
         if self.wire not in ("fp32", "bf16"):
             raise ValueError(f"P2P wire type must be fp32 or bf16, got {self.wire!r}")
-        self.out = torch.zeros_like(grad)
-        self.flags = torch.zeros(N_SLOTS * N_KINDS * MAX_RANKS, dtype=torch.int32, device=dev)
+        self.timeout_ms = int(os.environ.get("DRN_P2P_TIMEOUT_MS", "60000"))
+        # fault injection (tests): "rank:bucket" -- that rank never launches that bucket's reduce,
+        # i.e. never publishes it (eager steps only; a stuck peer as the other ranks see it)
+        wh = os.environ.get("DRN_FAULT_P2P_WITHHOLD", "")
+        self.withhold = int(wh.split(":")[1]) if wh and int(wh.split(":")[0]) == self.rank else -1
+        self._bufs = [_DeviceBuffer(self.L, grad.numel(), torch.float32, dev),
+                      _DeviceBuffer(self.L, N_SLOTS * N_KINDS * MAX_RANKS, torch.int32, dev)]
+        self.out = self._bufs[0].tensor
+        self.flags = self._bufs[1].tensor
         self.epoch = torch.zeros(1, dtype=torch.int32, device=dev)
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        # pinned host copy of the error word, refreshed by every step's end_step() (graph too)
+        self.err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         # the tensor the peers read: the fp32 gradient itself, or its bf16 wire shadow
         self.shadow = torch.zeros(grad.numel(), dtype=torch.bfloat16, device=dev) if self.wire == "bf16" else None
         src = self.shadow if self.shadow is not None else grad
@@ -171,6 +215,7 @@ class P2PAllReduce:
         a.err = self.err.data_ptr()
         a.n = hi - lo
         a.world, a.rank, a.slot = self.world, self.rank, slot
+        a.timeout_ms = self.timeout_ms
         return a
 
     @staticmethod
@@ -189,6 +234,8 @@ class P2PAllReduce:
         shadow there) then ONE kernel on the comm stream publishes it, polls for the peers without
         blocking the rest of this rank's backward pass, and reduces."""
         assert (hi - lo) % 4 == 0 and lo % 4 == 0 and i + 1 < N_SLOTS
+        if i == self.withhold:
+            return  # fault injection: this rank never publishes bucket i
         a = self._args(lo, hi, i + 1)
         cur = torch.cuda.current_stream()
         bf16 = self.shadow is not None
@@ -209,17 +256,38 @@ class P2PAllReduce:
 
     def end_step(self):
         """All buckets reduced on this rank: order the compute stream after the reductions (the
-        DONE publish happens at the next step's boundary launch)."""
-        torch.cuda.current_stream().wait_stream(self.comm)
+        DONE publish happens at the next step's boundary launch) and queue the copy of the error
+        word into pinned host memory (read by poll() without a device sync)."""
+        cur = torch.cuda.current_stream()
+        cur.wait_stream(self.comm)
+        self.err_host.copy_(self.err, non_blocking=True)
+
+    @staticmethod
+    def _raise(e: int):
+        what = {1: "a bucket's READY", 2: "the step boundary's DONE", 3: "a two-shot RS_DONE"}.get(e, "a peer")
+        raise RuntimeError(f"P2P all-reduce timed out waiting for {what} (code {e}): a peer rank is gone or "
+                           f"stuck; the step's update was not applied")
+
+    def poll(self):
+        """Non-blocking: raise if the error word of an already completed step is set (at most a
+        step or two behind the host; the update of any failed step was skipped on the device)."""
+        e = int(self.err_host[0])
+        if e:
+            self._raise(e)
 
     def check(self):
-        """Raise if a device-side wait timed out (a peer never arrived)."""
+        """Synchronous: raise if any device-side wait so far timed out (before a checkpoint)."""
         e = int(self.err.item())
         if e:
-            raise RuntimeError(f"P2P all-reduce timed out waiting for peers (code {e})")
+            self._raise(e)
 
     def close(self):
         h = _hip()
         for p in self._opened:
             h.hipIpcCloseMemHandle(ctypes.c_void_p(p))
         self._opened = []
+        if torch.cuda.is_available():
+            torch.cuda.synchronize(self.grad.device)
+        for b in self._bufs:
+            b.release()
+        self._bufs = []

@@ -868,7 +868,10 @@ class Executor:
             self._tail_ev = None
             self._join()
 
-    def apply_gradients(self, grad_scale: float = 1.0, grad: Optional[torch.Tensor] = None):
+    def apply_gradients(self, grad_scale: float = 1.0, grad: Optional[torch.Tensor] = None,
+                        skip: Optional[torch.Tensor] = None):
+        """Fused SGD-momentum + weight-layout refresh. skip: optional device int32 word; when it
+        is non-zero at run time no parameter or momentum changes (the P2P error word)."""
         P = self.P
         g = P.grad if grad is None else grad
         if self._tail_ev is not None and grad is None:
@@ -878,16 +881,16 @@ class Executor:
             torch.cuda.current_stream(self.device).wait_event(ev)
             wb = P.wbf16[hi:] if P.wbf16 is not None else None
             self.be.sgd_momentum(P.master[hi:], P.momentum[hi:], g[hi:], wb, self.lr_t, self.mom, self.wd,
-                                 grad_scale)
+                                 grad_scale, skip)
             self.refresh_dgrad_weights(stem=False)  # (the stem's weights are not updated yet)
             self.join_grads()
             wb = P.wbf16[:hi] if P.wbf16 is not None else None
             self.be.sgd_momentum(P.master[:hi], P.momentum[:hi], g[:hi], wb, self.lr_t, self.mom, self.wd,
-                                 grad_scale)
+                                 grad_scale, skip)
             self._repack_stem()
             return
         self.join_grads()
-        self.be.sgd_momentum(P.master, P.momentum, g, P.wbf16, self.lr_t, self.mom, self.wd, grad_scale)
+        self.be.sgd_momentum(P.master, P.momentum, g, P.wbf16, self.lr_t, self.mom, self.wd, grad_scale, skip)
         self.refresh_dgrad_weights()
 
     def sgd_range(self, lo: int, hi: int, grad_scale: float, grad: Optional[torch.Tensor] = None):

@@ -137,16 +137,19 @@ class ImagenetFeeder(_StagedFeeder):
     def _stage_item(self, item):
         packed, desc, labels = item
         n = int(packed.numel() if isinstance(packed, torch.Tensor) else packed.size)
+        # a pinned loader hands desc as a raw-byte tensor, labels as an int32 tensor
+        desc_bytes = desc if isinstance(desc, torch.Tensor) else desc.view(np.uint8)
         if not self.gpu:
-            self.h_packed, self.h_desc = packed, desc
-            self.d_lab.copy_(torch.from_numpy(labels))
+            self.h_packed = packed
+            self.h_desc = desc.numpy().view(self.inet.IMG_DESC) if isinstance(desc, torch.Tensor) else desc
+            self.d_lab.copy_(_as_tensor(labels))
             return
         if n > self.d_buf.numel():
             # stream-ordered reallocation: the old buffer is released only after the main
             # stream's last reader of it (the previous preprocess) is done
             torch.cuda.current_stream(self.ex.device).synchronize()
             self.d_buf = torch.empty(int(n * 1.25), dtype=torch.uint8, device=self.ex.device)
-        self._stage([(self.d_buf[:n], packed), (self.d_desc, desc.view(np.uint8)), (self.d_lab, labels)])
+        self._stage([(self.d_buf[:n], packed), (self.d_desc, desc_bytes), (self.d_lab, labels)])
 
     def _consume(self):
         if self.gpu:

@@ -9,7 +9,8 @@
   StopAtStepHook  StopAtStepHook(last_step=train_steps) (the reference CIFAR main never stops:
                   SURVEY Q5; here --train_steps is honoured).
   FaultInjectHook test hook: hard-exits one rank at a given step (restart/resume tests).
-  ProfileHook     roctx ranges + torch.profiler trace for --profile_steps=a:b.
+  ProfileHook     roctx ranges (one per step, and the data / fwd / bwd / comm / optimizer phases
+                  inside it) + torch.profiler trace for --profile_steps=a:b.
 """
 from __future__ import annotations
 
@@ -98,6 +99,7 @@ class CheckpointHook(Hook):
     """Time-based checkpoints (MonitoredTrainingSession save_checkpoint_secs) + one at the end.
     `agree` (sharded optimizer: the hook runs on every rank and the save is collective) turns the
     chief's timer decision into every rank's decision."""
+    writes_checkpoint = True  # skipped by the session's end-of-run after a failed step
 
     def __init__(self, save_secs: float, save_fn, agree=None):
         self.secs = save_secs
@@ -157,6 +159,7 @@ class ProfileHook(Hook):
         self.prof = None
         from ..utils import profiler
         self.roctx = profiler.Roctx()
+        profiler.enable_phases(True)  # data / fwd / bwd / comm / optimizer ranges inside each step
 
     def before_step(self, sess, step):
         if step == self.a:

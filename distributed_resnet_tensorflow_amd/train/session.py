@@ -21,6 +21,7 @@ from ..parallel.engine import DataParallelEngine
 from ..runtime.executor import Executor
 from ..runtime.graph import SegmentedStepGraph, StepGraph
 from ..runtime.state import export_state, import_state
+from ..utils.profiler import enable_phases, phase
 from .hooks import Hook
 
 log = logging.getLogger("drn")
@@ -86,6 +87,10 @@ class TrainingSession:
         self._graph: Optional[StepGraph] = None
         self._metrics_cache = None
         self.cur_lr = float("nan")
+        # set when a step's gradient exchange failed: no further checkpoint may be written
+        self.failed: Optional[str] = None
+        if os.environ.get("DRN_ROCTX") == "1":
+            enable_phases(True)
 
     # -- state -----------------------------------------------------------------------------------
     @property
@@ -111,6 +116,10 @@ class TrainingSession:
             self.engine.gather_state()
         if self.saver is None:
             return None
+        if self.failed:
+            raise RuntimeError(f"refusing to checkpoint after a failed step: {self.failed}")
+        if self.engine is not None:
+            self._guard(self.engine.check_errors)  # every queued step's exchange succeeded
         step = self.global_step if step is None else step
         extra = dict(self.data_state)
         tensors = export_state(self.ex, extra)
@@ -121,15 +130,21 @@ class TrainingSession:
     # -- stepping ----------------------------------------------------------------------------------
     def _step_body(self):
         ex = self.ex
-        ex.forward(train=True)
+        with phase("fwd"):
+            ex.forward(train=True)
         if self.engine is not None:
             self.engine.begin_step()
-            ex.backward()
-            g = self.engine.finish()
-            self.engine.apply_gradients(g, 1.0 / self.world)
+            with phase("bwd"):  # (bucket all-reduces are issued from inside the backward pass)
+                ex.backward()
+            with phase("comm"):
+                g = self.engine.finish()
+            with phase("optimizer"):
+                self.engine.apply_gradients(g, 1.0 / self.world)
         else:
-            ex.backward(defer_tail=not ex.check_nan)
-            ex.apply_gradients()
+            with phase("bwd"):
+                ex.backward(defer_tail=not ex.check_nan)
+            with phase("optimizer"):
+                ex.apply_gradients()
 
     def step(self):
         """One synchronous training step on the batch already in ex.images / ex.labels."""
@@ -142,12 +157,28 @@ class TrainingSession:
                 else:
                     self._graph = StepGraph(self._step_body, warmup=1)
             else:
-                self._graph.replay()
+                if self.engine is not None:
+                    self.engine.replay_begin()
+                with phase("step (graph replay)"):
+                    self._graph.replay()
+                if self.engine is not None:
+                    self.engine.replay_end()
         else:
             self._step_body()
         self.lr.after_step(self.ex.P.global_step)
         self.ex.P.global_step += 1
         self._metrics_cache = None
+        if self.engine is not None:
+            self._guard(self.engine.poll_errors)
+
+    def _guard(self, fn):
+        """Run an error check; on failure mark the session failed (no checkpoint after it)."""
+        try:
+            fn()
+        except RuntimeError as e:
+            self.failed = str(e)
+            log.error("step failed: %s", e)
+            raise
 
     def metrics(self) -> dict:
         """Loss / precision / lr of the last step, plus the gradient exchange's
@@ -158,8 +189,7 @@ class TrainingSession:
             m["learning_rate"] = self.cur_lr
             if self.engine is not None:
                 m.update(self.engine.stats())
-                if self.engine.p2p is not None:
-                    self.engine.p2p.check()
+                self._guard(self.engine.check_errors)
             if self.device.type == "cuda":
                 free, total = torch.cuda.mem_get_info(self.device)
                 m["hbm_used_gb"] = (total - free) / 1e9
@@ -173,8 +203,9 @@ class TrainingSession:
             h.begin(self)
         try:
             while not any(h.should_stop(self.global_step) for h in hooks):
-                if not feeder.next():
-                    break
+                with phase("data"):
+                    if not feeder.next():
+                        break
                 self.data_state = feeder.state()
                 for h in hooks:
                     h.before_step(self, self.global_step)
@@ -185,6 +216,9 @@ class TrainingSession:
             if self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
             for h in hooks:
+                if self.failed and getattr(h, "writes_checkpoint", False):
+                    log.error("no final checkpoint: %s", self.failed)
+                    continue
                 h.end(self)
             if self.saver is not None:
                 self.saver.wait()

@@ -29,6 +29,40 @@ class Roctx:
             self.lib.roctxRangePop()
 
 
+_ROCTX = None
+_PHASES_ON = False
+
+
+def enable_phases(on: bool = True) -> None:
+    """Turn the per-step phase ranges on (ProfileHook / DRN_ROCTX=1). Off, phase() costs one
+    attribute check."""
+    global _ROCTX, _PHASES_ON
+    if on and _ROCTX is None:
+        _ROCTX = Roctx()
+    _PHASES_ON = bool(on) and _ROCTX is not None and _ROCTX.lib is not None
+
+
+class phase:
+    """`with phase("fwd"):` -- a roctx range (rocprofv3 --marker-trace) around one phase of the
+    training step (data / fwd / bwd / comm / optimizer). Host-side ranges: they
+    bracket the enqueue of the phase's kernels (for device time, pair them with --kernel-trace)."""
+    __slots__ = ("name", "on")
+
+    def __init__(self, name: str):
+        self.name = name
+        self.on = _PHASES_ON
+
+    def __enter__(self):
+        if self.on:
+            _ROCTX.push(self.name)
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            _ROCTX.pop()
+        return False
+
+
 def model_report(spec) -> str:
     lines = [f"model {spec.name}: {len(spec.trainable_variables())} trainable variables, "
              f"total_params: {spec.num_params():,}",

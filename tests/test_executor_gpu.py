@@ -221,3 +221,44 @@ def test_precision_fp32_reference_backend_on_gpu():
     # test_step_matches_reference does
     ga, gb = out["fp32"][1], out["bf16"][1]
     assert torch.nn.functional.cosine_similarity(ga, gb, dim=0).item() > 0.99
+
+
+@pytest.mark.parametrize("which", ["cifar20", "in18"])
+def test_bn_moving_statistics_track_oracle_over_training(which):
+    """20 training steps on the HIP kernels vs the fp32 autograd oracle (models/oracle.py) fed the
+    SAME batches and, every step, the HIP executor's current weights rounded to bf16: every BN's
+    moving mean / moving variance (TF fused-BN update, decay 0.997, unbiased batch variance;
+    reference resnet_model_official.py:37-48, resnet_model.py:118-121) must agree to 2e-2
+    relative -- the statistics the eval path (resnet_cifar_eval.py:110-123) normalises with."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from distributed_resnet_tensorflow_amd.models import oracle
+    spec, N = {"cifar20": (cifar_resnet_v2(20), 32),
+               "in18": (imagenet_resnet_v2(18, num_classes=10, image_size=64), 16)}[which]
+    torch.manual_seed(3)
+    h = Executor(spec, N, HipBackend(), "cuda", seed=7, weight_decay=2e-4)
+    st = oracle.state_from_store(h.P)  # initial moving statistics (0 / 1), updated by the oracle
+    st0 = {k: (m.clone(), v.clone()) for k, (m, v) in st.items()}
+    for step in range(20):
+        imgs = (torch.randn(N, spec.image_size, spec.image_size, 3) * 1.5 + 0.2).bfloat16()
+        labels = torch.randint(0, spec.num_classes, (N,), dtype=torch.int32)
+        p = {k: v.detach().bfloat16().float().cpu() for k, v in oracle.params_from_store(h.P, False).items()}
+        with torch.no_grad():
+            oracle.forward(spec, p, st, imgs.float(), training=True)
+        h.images.zero_()
+        h.images[..., :3] = imgs.cuda()
+        h.labels.copy_(labels.cuda())
+        h.train_step(lr=0.1)
+    torch.cuda.synchronize()
+    # compare what the 20 updates ADDED (the initial 0 / 1 decays by 0.997^20 on both sides and
+    # would otherwise dominate the variance's norm)
+    d20 = 0.997 ** 20
+    worst = []
+    for name in h.P.bn_slots:
+        m, v = h.P.moving(name)
+        m0, v0 = st0[name]
+        em = rel(m.cpu() - d20 * m0, st[name][0] - d20 * m0)
+        ev = rel(v.cpu() - d20 * v0, st[name][1] - d20 * v0)
+        worst.append((max(em, ev), name, em, ev))
+    worst.sort(reverse=True)
+    assert worst[0][0] < 2e-2, worst[:5]

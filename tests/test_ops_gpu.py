@@ -89,8 +89,13 @@ GLDS_CASES = [
 ]
 
 
+N_GLDS = 31                              # one-tile LDS-DMA configurations (DRN_GLDS_NCFG)
+BK32 = set(range(17, 23)) | {25, 27, 28, 29, 30}  # 32-deep stages: C % 32 == 0 suffices
+BIG = set(range(25, 31))                 # 8-wave big tiles: no row-staged narrow inputs
+
+
 @pytest.mark.parametrize("case", GLDS_CASES)
-@pytest.mark.parametrize("cfg", list(range(25)))
+@pytest.mark.parametrize("cfg", list(range(N_GLDS)))
 @pytest.mark.parametrize("pro", [False, True])
 def test_conv_fwd_glds_configs(hip, ref, case, cfg, pro):
     """Every tile/pipeline configuration of the LDS-DMA conv kernel vs the fp32 reference,
@@ -114,7 +119,7 @@ def test_conv_fwd_glds_configs(hip, ref, case, cfg, pro):
     assert hip.L.drn_conv_glds_ok(a) == 1 and a.stats_rep == 3
     a.cfg = cfg
     narrow = C in (8, 16)                # row-staged: the 64-deep-stage configurations only
-    if (C % 64 and not narrow and (cfg < 17 or cfg > 22)) or (narrow and 17 <= cfg <= 22):
+    if (C % 64 and not narrow and cfg not in BK32) or (narrow and (cfg in BK32 or cfg in BIG)):
         assert hip.L.drn_conv_fwd2(ctypes.byref(a), hip.zero_page.data_ptr(), hip.stream()) != 0
         return
     hip.launch_conv(a)
@@ -134,7 +139,7 @@ def test_conv_glds_out_map(hip, ref):
     om = OutMap(P=P, Q=P, stride=2, oh=1, ow=0)
     y_ref = torch.zeros(N, 2 * P, 2 * P, K)
     ref.conv_fwd(x.float(), w.float(), y_ref, ConvGeom(1, 0, 0), out_map=om)
-    for cfg in range(23):
+    for cfg in list(range(23)) + sorted(BIG):
         y = torch.zeros(N, 2 * P, 2 * P, K, dtype=torch.bfloat16, device="cuda")
         a = hip.conv_args(x.cuda(), w.cuda(), y, ConvGeom(1, 0, 0), out_map=om)
         a.cfg = cfg
@@ -143,7 +148,7 @@ def test_conv_glds_out_map(hip, ref):
         assert rel(y, y_ref) < 1e-2, cfg
 
 
-@pytest.mark.parametrize("cfg", [100, 0, 3, 6, 13, 18])
+@pytest.mark.parametrize("cfg", [100, 0, 3, 6, 13, 18, 25, 27])
 @pytest.mark.parametrize("size", [5, 4])
 def test_conv_out_fill(hip, ref, cfg, size):
     """Single-phase strided output (1x1 stride-2 projection data gradient) with out_fill: the
@@ -171,7 +176,7 @@ def test_conv_out_fill(hip, ref, cfg, size):
     assert float(y.float()[:, :, 1::2].abs().max()) == 0.0
 
 
-@pytest.mark.parametrize("cfg", [100, 0, 3, 6])
+@pytest.mark.parametrize("cfg", [100, 0, 3, 6, 25, 28])
 def test_conv_fused_bn_bwd_reduce(hip, ref, cfg):
     """Data-gradient conv with the fused BN-backward epilogue (ReLU mask + sum g, sum g*xhat)."""
     torch.manual_seed(11)
