@@ -13,8 +13,18 @@
 
 namespace drn {
 
+// gradient element type: fp32 (local / fp32-wire gradients) or bf16 (the all-reduced bf16 wire
+// buffer, consumed directly: no cast-back pass, half the gradient bytes)
+__device__ __forceinline__ float4 grad4(const float* g, int64_t i) { return reinterpret_cast<const float4*>(g)[i]; }
+__device__ __forceinline__ float4 grad4(const bf16_t* g, int64_t i) {
+  const uint2 u = reinterpret_cast<const uint2*>(g)[i];
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+
+template <typename G>
 __global__ __launch_bounds__(256) void sgd_momentum_kernel(float* __restrict__ w, float* __restrict__ m,
-                                                           const float* __restrict__ g, bf16_t* __restrict__ wb,
+                                                           const G* __restrict__ g, bf16_t* __restrict__ wb,
                                                            int64_t n4, const float* __restrict__ lr_ptr, float mu,
                                                            float wd, float grad_scale, const int* __restrict__ skip) {
   // skip: the step's gradient exchange failed (P2P error word): apply no update at all
@@ -23,7 +33,7 @@ __global__ __launch_bounds__(256) void sgd_momentum_kernel(float* __restrict__ w
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
     float4 wv = reinterpret_cast<float4*>(w)[i];
     float4 mv = reinterpret_cast<float4*>(m)[i];
-    const float4 gv = reinterpret_cast<const float4*>(g)[i];
+    const float4 gv = grad4(g, i);
     float gg;
     gg = gv.x * grad_scale + wd * wv.x; mv.x = mu * mv.x + gg; wv.x -= lr * mv.x;
     gg = gv.y * grad_scale + wd * wv.y; mv.y = mu * mv.y + gg; wv.y -= lr * mv.y;
@@ -131,12 +141,18 @@ static inline int grid_for(int64_t n) {
 
 }  // namespace drn
 
-// skip (nullable device int): when *skip != 0 at run time the launch changes nothing
-DRN_API int drn_sgd_momentum(float* w, float* m, const float* g, void* w_bf16, int64_t n, const float* lr_ptr,
-                             float momentum, float wd, float grad_scale, const int* skip, hipStream_t s) {
+// skip (nullable device int): when *skip != 0 at run time the launch changes nothing;
+// g_bf16: the gradient is bf16 (the all-reduced bf16 wire buffer), else fp32
+DRN_API int drn_sgd_momentum(float* w, float* m, const void* g, int g_bf16, void* w_bf16, int64_t n,
+                             const float* lr_ptr, float momentum, float wd, float grad_scale, const int* skip,
+                             hipStream_t s) {
   if (n % 4) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(drn::sgd_momentum_kernel, dim3(drn::grid_for(n / 4)), dim3(256), 0, s, w, m, g,
-                     (bf16_t*)w_bf16, n / 4, lr_ptr, momentum, wd, grad_scale, skip);
+  if (g_bf16)
+    hipLaunchKernelGGL(drn::sgd_momentum_kernel<bf16_t>, dim3(drn::grid_for(n / 4)), dim3(256), 0, s, w, m,
+                       (const bf16_t*)g, (bf16_t*)w_bf16, n / 4, lr_ptr, momentum, wd, grad_scale, skip);
+  else
+    hipLaunchKernelGGL(drn::sgd_momentum_kernel<float>, dim3(drn::grid_for(n / 4)), dim3(256), 0, s, w, m,
+                       (const float*)g, (bf16_t*)w_bf16, n / 4, lr_ptr, momentum, wd, grad_scale, skip);
   return (int)hipGetLastError();
 }
 

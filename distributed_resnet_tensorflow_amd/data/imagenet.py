@@ -202,6 +202,68 @@ class _Shard:
         return frame[12:12 + ln]
 
 
+_WORKER_SHARDS: dict = {}
+_CHUNK = 8  # records per decode-process task
+_SHM_PREFIX = "drn_dec_"
+_SEQ = 0
+
+
+def _decode_in_worker(path: str, r: int):
+    """Decode-worker-process side of ImagenetLoader(workers="process"): read record r of the
+    shard (its own memory map, CRC-checked), parse the Example, decode the JPEG. Module level
+    and torch-free so a spawned worker imports only numpy / PIL / this package's codecs."""
+    sh = _WORKER_SHARDS.get(path)
+    if sh is None:
+        sh = _WORKER_SHARDS[path] = _Shard(path)
+    ex = parse_example(sh.record(r))
+    img = decode_image(ex["image/encoded"][0])
+    # the pixels travel through a shared-memory segment, not the result pipe: pickling ~0.5 MB
+    # per image through the pool's single result thread capped the parent near 1k img/s. The
+    # segment is named after the loader's process (cleanup of leftovers: _shm_cleanup) and is
+    # owned by the parent, which unlinks it after copying: not tracked here.
+    from multiprocessing import resource_tracker, shared_memory
+    global _SEQ
+    _SEQ += 1
+    seg = shared_memory.SharedMemory(name=f"{_SHM_PREFIX}{os.getppid()}_{os.getpid()}_{_SEQ}", create=True,
+                                     size=max(1, img.nbytes))
+    resource_tracker.unregister(seg._name, "shared_memory")
+    np.ndarray(img.shape, np.uint8, buffer=seg.buf)[...] = img
+    name = seg.name
+    seg.close()
+    return (name, img.shape), int(ex.get("image/class/label", [-1])[0])
+
+
+def _shm_cleanup(pid: int) -> None:
+    """Unlink every decode segment created for loader process `pid` that is still in /dev/shm
+    (batches decoded but never consumed when the loader stops)."""
+    for f in glob.glob(f"/dev/shm/{_SHM_PREFIX}{pid}_*"):
+        try:
+            os.unlink(f)
+        except OSError:
+            pass
+
+
+def _decode_chunk_in_worker(items):
+    """Several records per task (fewer pool round trips): [(path, r)] -> [((shm, shape), label)]."""
+    return [_decode_in_worker(p, r) for p, r in items]
+
+
+class _ShmImage:
+    """A decoded image left in a shared-memory segment by a decode worker: attached on the
+    loader thread, copied into the batch buffer, then unlinked."""
+    __slots__ = ("seg", "arr")
+
+    def __init__(self, name: str, shape):
+        from multiprocessing import shared_memory
+        self.seg = shared_memory.SharedMemory(name=name)
+        self.arr = np.ndarray(shape, np.uint8, buffer=self.seg.buf)
+
+    def release(self):
+        self.arr = None
+        self.seg.close()
+        self.seg.unlink()
+
+
 class ImagenetLoader:
     """Background pipeline producing packed decoded batches:
     (packed uint8 buffer, IMG_DESC array [B], int32 labels [B]).
@@ -213,11 +275,18 @@ class ImagenetLoader:
     any image. Crop/flip geometry of batch b comes from an RNG seeded with (seed, rank, b). Each
     batch carries the position after it; `state()` reports the position after the last batch
     handed out. With `pin=True` batches are packed straight into page-locked tensors.
+
+    workers="thread" decodes in a thread pool; "process" in spawned worker processes. JPEG
+    decoding holds the GIL for part of each image (colour conversion, array copies): measured on
+    8 cores (scripts/imagenet_input_bench.py, profiles/r3_imagenet_input_bench.txt) threads
+    saturate near 1.3k img/s while processes scale ~linearly (~350 img/s per core for 500x375
+    JPEGs), so training uses processes.
     """
 
     def __init__(self, data_dir: str, batch_size: int, is_training: bool, seed: int = 0, rank: int = 0,
                  world: int = 1, num_threads: int = 8, prefetch: int = 3, num_epochs: Optional[int] = None,
-                 epoch: int = 0, cursor: int = 0, batch_index: int = 0, pin: bool = False, pin_device=None):
+                 epoch: int = 0, cursor: int = 0, batch_index: int = 0, pin: bool = False, pin_device=None,
+                 workers: str = "thread"):
         files = filenames(is_training, data_dir)
         if is_training and world > 1:
             files = files[rank::world] or files
@@ -229,7 +298,18 @@ class ImagenetLoader:
         self.pin, self.pin_device = pin, _device_index(pin_device) if pin else None
         self._error: Optional[BaseException] = None
         self.epoch, self.cursor, self.batch_index = epoch, cursor, batch_index
-        self.pool = ThreadPoolExecutor(max_workers=max(1, num_threads))
+        if workers not in ("thread", "process"):
+            raise ValueError(f"decode workers must be 'thread' or 'process', got {workers!r}")
+        self.workers = workers
+        if workers == "process":
+            import atexit
+            import multiprocessing as mp
+            from concurrent.futures import ProcessPoolExecutor
+            # spawn: never fork a process that holds a GPU context
+            self.pool = ProcessPoolExecutor(max_workers=max(1, num_threads), mp_context=mp.get_context("spawn"))
+            atexit.register(_shm_cleanup, os.getpid())
+        else:
+            self.pool = ThreadPoolExecutor(max_workers=max(1, num_threads))
         self.q: "queue.Queue" = queue.Queue(maxsize=max(1, prefetch))
         self._stop = threading.Event()
         self._t = threading.Thread(target=self._run, daemon=True)
@@ -286,7 +366,13 @@ class ImagenetLoader:
             batch.append((s, r))
             if len(batch) < self.bs:
                 continue
-            inflight.append(([self.pool.submit(self._decode, pos) for pos in batch], epoch, cursor))
+            if self.workers == "process":
+                items = [(self.shards[s].path, r) for s, r in batch]
+                futs = [self.pool.submit(_decode_chunk_in_worker, items[i:i + _CHUNK])
+                        for i in range(0, len(items), _CHUNK)]
+            else:
+                futs = [self.pool.submit(self._decode, pos) for pos in batch]
+            inflight.append((futs, epoch, cursor))
             batch = []
             if len(inflight) > 1:
                 yield inflight.pop(0)
@@ -313,7 +399,13 @@ class ImagenetLoader:
                 import torch
                 torch.cuda.set_device(self.pin_device)
             for futs, epoch, cursor in self._batches():
-                decoded = [f.result() for f in futs]
+                shm = []
+                if self.workers == "process":
+                    decoded = [d for f in futs for d in f.result()]
+                    shm = [_ShmImage(*ref) for ref, _ in decoded]
+                    decoded = [(m.arr, lab) for m, (_, lab) in zip(shm, decoded)]
+                else:
+                    decoded = [f.result() for f in futs]
                 rng = np.random.default_rng([self.seed, self.rank, 99, b])
                 total = sum(d[0].size for d in decoded)
                 packed, flat = self._host(total, np.uint8)
@@ -328,6 +420,9 @@ class ImagenetLoader:
                     desc[i] = (off, h, w, rh, rw, cy, cx, flip, 0)
                     labels[i] = lab
                     off += img.size
+                decoded = None
+                for m in shm:
+                    m.release()
                 b += 1
                 # pin=True: the page-locked tensors themselves (desc as raw IMG_DESC bytes), so the
                 # caching host allocator tracks their async copies
@@ -369,7 +464,9 @@ class ImagenetLoader:
         except queue.Empty:
             pass
         self._t.join(timeout=2)
-        self.pool.shutdown(wait=False)
+        self.pool.shutdown(wait=self.workers == "process", cancel_futures=True)
+        if self.workers == "process":
+            _shm_cleanup(os.getpid())
 
 
 def write_fake_imagenet(dirpath: str, shards: int = 2, per_shard: int = 8, is_training: bool = True,

@@ -235,9 +235,13 @@ def define_reference_flags(flag_values: FlagValues = FLAGS, **defaults) -> FlagV
     I("fault_inject_rank", 0, "Rank that --fault_inject_step applies to.", fv)
     B("hip_graph", True, "Capture the single-GPU training step in a HIP graph.", fv)
     I("seed", 0, "Random seed (weights, data order, augmentation).", fv)
+    Fl("lr_schedule_scale", 1.0, "Scale of every step boundary of the reference LR schedule (1.0 = the "
+       "reference; e.g. 0.05 decays the CIFAR LR at 2k/3k/4k steps for short runs).", fv)
     I("eval_interval_secs", 60, "Eval poller period (reference sleeps 60 s).", fv)
     Fl("weight_decay", None, "Override the dataset's weight decay (CIFAR 2e-4, ImageNet 1e-4).", fv)
     I("num_workers", 2, "Host data-loader worker threads.", fv)
+    S("input_workers", "process", "ImageNet JPEG decode workers: process (spawned decode processes, scales with "
+      "cores) or thread (a thread pool; JPEG decode partly holds the GIL).", fv)
     S("master_addr", "", "Rendezvous address override (default MASTER_ADDR or worker_hosts[0]).", fv)
     for k, v in defaults.items():
         fv.set_default(k, v)

@@ -108,7 +108,7 @@ _SIGS = {
     "drn_colsum": ([c_p, c_int, c_int, c_p, c_f, c_int, c_p], c_int),
     "drn_maxpool_fwd": ([c_p, c_p, c_p] + [c_int] * 10 + [c_p, c_int, c_p], c_int),
     "drn_maxpool_bwd": ([c_p, c_p, c_p] + [c_int] * 10 + [c_p], c_int),
-    "drn_sgd_momentum": ([c_p, c_p, c_p, c_p, c_i64, c_p, c_f, c_f, c_f, c_p, c_p], c_int),
+    "drn_sgd_momentum": ([c_p, c_p, c_p, c_int, c_p, c_i64, c_p, c_f, c_f, c_f, c_p, c_p], c_int),
     "drn_cast_bf16": ([c_p, c_p, c_i64, c_p], c_int),
     "drn_stem_pack_input": ([c_p, c_p, c_int, c_int, c_p], c_int),
     "drn_stem_pack_weights": ([c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p], c_int),

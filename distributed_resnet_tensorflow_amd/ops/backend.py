@@ -668,9 +668,10 @@ class HipBackend(_Common):
     def sgd_momentum(self, w, m, g, wb, lr_t, momentum, wd, grad_scale, skip=None):
         """Fused SGD-momentum; skip = optional device int32 word: the launch changes nothing when
         it holds a non-zero value at run time (a failed P2P gradient exchange)."""
-        _lib.check(self.L.drn_sgd_momentum(w.data_ptr(), m.data_ptr(), g.data_ptr(), _ptr(wb), w.numel(),
-                                           lr_t.data_ptr(), float(momentum), float(wd), float(grad_scale),
-                                           _ptr(skip), self.stream()), "drn_sgd_momentum")
+        assert g.dtype in (torch.float32, torch.bfloat16) and g.numel() == w.numel()
+        _lib.check(self.L.drn_sgd_momentum(w.data_ptr(), m.data_ptr(), g.data_ptr(), int(g.dtype == torch.bfloat16),
+                                           _ptr(wb), w.numel(), lr_t.data_ptr(), float(momentum), float(wd),
+                                           float(grad_scale), _ptr(skip), self.stream()), "drn_sgd_momentum")
 
     def cast_bf16(self, x, y):
         _lib.check(self.L.drn_cast_bf16(x.data_ptr(), y.data_ptr(), x.numel(), self.stream()), "drn_cast_bf16")
@@ -1010,7 +1011,7 @@ class RefBackend(_Common):
         if skip is not None and int(skip.reshape(-1)[0]) != 0:
             return
         lr = float(lr_t.reshape(-1)[0])
-        gg = g * grad_scale + wd * w
+        gg = g.to(w.dtype) * grad_scale + wd * w
         m.mul_(momentum).add_(gg)
         w.sub_(lr * m)
         if wb is not None and wb.data_ptr() != w.data_ptr():

@@ -77,8 +77,8 @@ def _headers_mtime() -> float:
     return max((h.stat().st_mtime for h in hs), default=0.0)
 
 
-def _compile(src: Path, extra: list[str]) -> Path:
-    obj = OBJ_DIR / (src.stem + ".o")
+def _compile(src: Path, extra: list[str], obj_dir: Optional[Path] = None) -> Path:
+    obj = (obj_dir or OBJ_DIR) / (src.stem + ".o")
     if obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, _headers_mtime()):
         return obj
     # DRN_CONV_TRACE=1: diagnostics build with the per-workgroup conv timeline
@@ -159,5 +159,28 @@ def build(force: bool = False, verbose: bool = True, extra: list[str] | None = N
     return LIB_PATH
 
 
+def build_variant(out_dir: str, extra: list[str]) -> Path:
+    """A diagnostics / A-B variant of the kernel library (e.g. extra=["-DDRN_CONV_TRACE"]) built
+    into out_dir/libdrn_kernels.so with its own objects; load it with DRN_KERNEL_LIB=<path>
+    (the source-stamp check is skipped for an explicit library)."""
+    out = Path(out_dir).resolve()
+    obj_dir = REPO / "build" / ("variant_" + out.name)  # objects stay out of the shipped tree
+    obj_dir.mkdir(parents=True, exist_ok=True)
+    srcs = sources()
+    with cf.ThreadPoolExecutor(max_workers=min(len(srcs), 8)) as ex:
+        objs = list(ex.map(lambda s: _compile(s, list(extra), obj_dir), srcs))
+    objs.append(_stamp_object())
+    lib = out / "libdrn_kernels.so"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib)] + [str(o) for o in objs]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"link failed:\n{res.stderr[-6000:]}")
+    return lib
+
+
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if "--variant" in sys.argv:  # --variant <out_dir> <hipcc flags...>
+        i = sys.argv.index("--variant")
+        print(build_variant(sys.argv[i + 1], sys.argv[i + 2:]))
+    else:
+        build(force="--force" in sys.argv)

@@ -109,8 +109,10 @@ class DataParallelEngine:
         self.zero1 = bool(shard_optimizer) and self.world > 1 and mode == "sync"
         if self.zero1 and self.wire != "fp32":
             raise ValueError("optimizer sharding reduce-scatters fp32 gradients (--allreduce_wire=fp32)")
-        # RCCL bf16 wire: a bf16 shadow of the flat gradient; each bucket is cast into it, reduced
-        # there, and cast back into the fp32 buffer after its collective completes
+        # RCCL bf16 wire: a bf16 shadow of the flat gradient; each bucket is cast into it by an
+        # in-tree kernel on the compute stream and all-reduced THERE, and the fused SGD reads the
+        # reduced bf16 buffer directly (no cast-back pass). The sum is accumulated in bf16 inside
+        # RCCL (rounding grows with the rank count; the P2P bf16 wire accumulates in fp32)
         self.wire_buf = None
         if self.wire == "bf16" and self.p2p is None and mode == "sync":
             self.wire_buf = torch.zeros(self.P.total, dtype=torch.bfloat16, device=self.P.grad.device)
@@ -204,7 +206,7 @@ class DataParallelEngine:
         t = (self.P.grad if buf is None else buf)[lo:hi]
         if self.wire_buf is not None and buf is None:
             w = self.wire_buf[lo:hi]
-            w.copy_(t)                         # fp32 -> bf16 (round to nearest even), stream-ordered
+            self.ex.be.cast_bf16(t, w)         # fp32 -> bf16 (RNE), in-tree kernel, stream-ordered
             self.works.append(dist.all_reduce(w, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
             self.launched[i] = True
             return
@@ -245,15 +247,13 @@ class DataParallelEngine:
             for w in self.works:
                 w.wait()
             self._done_works, self.works = self.works, []
-            if self.wire_buf is not None:      # bf16 sums back into the fp32 gradient buffer
-                self.P.grad.copy_(self.wire_buf)
             self.ex.grad_ready = None
             if self.p2p is not None:
                 self.p2p.end_step()
                 self._done()
                 return self.p2p.out
             self._done()
-            return self.P.grad
+            return self.wire_buf if self.wire_buf is not None else self.P.grad
         # delayed (async-PS analog): finish last step's exchange, start this step's
         self._mark(1)
         for w in self.works:

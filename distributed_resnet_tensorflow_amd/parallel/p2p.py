@@ -282,12 +282,16 @@ class P2PAllReduce:
             self._raise(e)
 
     def close(self):
+        """Collective teardown: unmap the peers' buffers, wait until every rank has done the
+        same (nobody maps this rank's exported memory any more), then free it."""
+        if torch.cuda.is_available():
+            torch.cuda.synchronize(self.grad.device)
         h = _hip()
         for p in self._opened:
             h.hipIpcCloseMemHandle(ctypes.c_void_p(p))
         self._opened = []
-        if torch.cuda.is_available():
-            torch.cuda.synchronize(self.grad.device)
+        if self.world > 1:
+            dist.barrier(group=self.group)
         for b in self._bufs:
             b.release()
         self._bufs = []

@@ -48,7 +48,12 @@ class LRSchedule:
         self.next_lr = self.fn(global_step)
 
 
-def for_dataset(dataset: str) -> LRSchedule:
-    if dataset == "imagenet":
-        return LRSchedule(imagenet_lr, 0.4)
-    return LRSchedule(cifar_lr, 0.1)
+def for_dataset(dataset: str, step_scale: float = 1.0) -> LRSchedule:
+    """The reference's schedule for `dataset`. step_scale (--lr_schedule_scale, an extension for
+    short runs: tests, smoke trainings) stretches / compresses every step boundary: 0.05 puts
+    the CIFAR decays at 2k / 3k / 4k steps instead of 40k / 60k / 80k. 1.0 = the reference."""
+    if step_scale <= 0:
+        raise ValueError(f"--lr_schedule_scale must be > 0, got {step_scale}")
+    base = imagenet_lr if dataset == "imagenet" else cifar_lr
+    fn = base if step_scale == 1.0 else (lambda step: base(int(step / step_scale)))
+    return LRSchedule(fn, 0.4 if dataset == "imagenet" else 0.1)

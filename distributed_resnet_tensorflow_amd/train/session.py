@@ -55,9 +55,22 @@ class TrainingSession:
         self.ex = Executor(spec, batch, self.be, self.device, seed=seed, weight_decay=weight_decay)
         self.lr = lr_schedule
         self.meta = meta or {}
+        # DRN_FORCE_DP=1: the data-parallel engine on a single-rank process group (profiling the
+        # multi-GPU step machinery -- comm streams, HW-queue use -- on one GPU)
+        dp = cluster.distributed or os.environ.get("DRN_FORCE_DP") == "1"
+        if dp and not cluster.distributed:
+            import torch.distributed as dist
+            if not dist.is_initialized():
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                os.environ.setdefault("MASTER_PORT", os.environ.get("DRN_FORCE_DP_PORT", "29541"))
+                if self.device.type == "cuda":
+                    dist.init_process_group("nccl", rank=0, world_size=1, device_id=self.device)
+                else:
+                    dist.init_process_group("gloo", rank=0, world_size=1)
+        self.dp = dp
         self.engine = DataParallelEngine(self.ex, bucket_mb=bucket_mb, mode=sync_mode, allreduce=allreduce, wire=wire,
                                          timeout_s=collective_timeout_s,
-                                         shard_optimizer=shard_optimizer) if cluster.distributed else None
+                                         shard_optimizer=shard_optimizer) if dp else None
         self.sharded = self.engine is not None and self.engine.zero1
         self.world = cluster.world
         self.ckpt_dir = checkpoint_dir
@@ -77,11 +90,11 @@ class TrainingSession:
         # collective is a kernel with device-side flags): also the whole step, comm included, in
         # one graph. Data parallel over RCCL: eager (measured faster than the chain
         # of per-segment graphs, SegmentedStepGraph, which DRN_DP_GRAPH=1 selects)
-        dp_ok = cluster.distributed and self.engine.mode == "sync" and not self.sharded
+        dp_ok = dp and self.engine.mode == "sync" and not self.sharded
         self.use_graph = use_graph and self.device.type == "cuda" and self.be.name == "hip" and (
-            not cluster.distributed or (dp_ok and self.engine.p2p is not None) or
+            not dp or (dp_ok and self.engine.p2p is not None) or
             (dp_ok and os.environ.get("DRN_DP_GRAPH") == "1"))
-        if cluster.distributed and not self.use_graph and self.device.type == "cuda":
+        if dp and not self.use_graph and self.device.type == "cuda":
             from ..parallel.engine import use_priority_main_stream
             use_priority_main_stream()  # eager DP step: critical path on its own HW queue
         self._graph: Optional[StepGraph] = None
@@ -222,5 +235,7 @@ class TrainingSession:
                 h.end(self)
             if self.saver is not None:
                 self.saver.wait()
-            if self.engine is not None:
+            if self.engine is not None and not self.failed:
+                # (after a failed exchange a peer may be gone or still mapping this rank's
+                # buffers: leave them to process exit instead of a collective teardown)
                 self.engine.close()

@@ -75,7 +75,7 @@ def make_feeder(FLAGS, ex, cluster, is_training: bool, data_state=None, batch=No
                                      num_threads=max(2, FLAGS.num_workers * 4),
                                      num_epochs=FLAGS.num_epochs if is_training else 1,
                                      epoch=int(ds.get("data_epoch", 0)), cursor=int(ds.get("data_cursor", 0)),
-                                     batch_index=int(ds.get("data_batch", 0)), **pin)
+                                     batch_index=int(ds.get("data_batch", 0)), workers=FLAGS.input_workers, **pin)
     return ImagenetFeeder(ex, loader, is_training)
 
 
@@ -102,7 +102,7 @@ def train(FLAGS, cluster=None):
         if cluster.is_chief:
             log.info("--sync_replicas=False: 1-step-delayed all-reduce (async-PS analog, staleness 1; not "
                      "bit-equivalent to TF asynchronous parameter servers)")
-    sess = TrainingSession(spec, FLAGS.batch_size, cluster, weight_decay=wd, lr_schedule=lr_mod.for_dataset(FLAGS.dataset),
+    sess = TrainingSession(spec, FLAGS.batch_size, cluster, weight_decay=wd, lr_schedule=lr_mod.for_dataset(FLAGS.dataset, FLAGS.lr_schedule_scale),
                            checkpoint_dir=FLAGS.log_root, max_to_keep=FLAGS.max_to_keep, seed=FLAGS.seed,
                            use_graph=FLAGS.hip_graph, sync_mode=sync_mode, bucket_mb=FLAGS.bucket_mb,
                            meta=_meta(FLAGS, spec), allreduce=FLAGS.allreduce, wire=FLAGS.allreduce_wire,

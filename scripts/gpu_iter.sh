@@ -8,7 +8,7 @@ K=${K:-""}
 export PYTHONPATH=$(pwd)
 mkdir -p "$OUT"
 if [ "$TESTS" != "none" ]; then
-  timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -q --timeout 240 --timeout-method thread \
+  timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -v --timeout 170 --timeout-method thread \
     ${K:+-k "$K"} > "$OUT/tests.log" 2>&1
   rc=$?
   tail -3 "$OUT/tests.log"

@@ -6,7 +6,7 @@ MI355X needs at the trained step rate (reference: 5 parallel map threads + prefe
 resnet_imagenet_main.py:158-183; VGG geometry vgg_preprocessing.py:284-333, which here runs on
 the GPU).
 
-    python scripts/imagenet_input_bench.py [--images 512] [--threads 1,2,4,8]
+    python scripts/imagenet_input_bench.py [--images 512] [--threads 1,2,4,8] [--workers thread,process]
 Prints one JSON line per configuration.
 """
 import argparse
@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--images", type=int, default=512)
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--threads", default="1,2,4,8")
+    ap.add_argument("--workers", default="thread,process")
     args = ap.parse_args()
     rng = np.random.default_rng(0)
     d = tempfile.mkdtemp(prefix="drn_inbench_")
@@ -63,17 +64,19 @@ def main():
         n += 1
     per_core = n / (time.perf_counter() - t0)
     print(json.dumps({"what": "decode_one_core", "jpeg": "500x375 q90", "img_per_s": round(per_core, 1)}), flush=True)
-    for nt in [int(t) for t in args.threads.split(",")]:
-        ld = inet.ImagenetLoader(d, args.batch, True, num_threads=nt, prefetch=3, num_epochs=None)
-        next(ld)  # warm-up batch
-        t0 = time.perf_counter()
-        nb = max(2, args.images // args.batch)
-        for _ in range(nb):
-            next(ld)
-        dt = time.perf_counter() - t0
-        ld.close()
-        print(json.dumps({"what": "loader", "threads": nt, "batch": args.batch,
-                          "img_per_s": round(nb * args.batch / dt, 1), "cpus": os.cpu_count()}), flush=True)
+    for workers in args.workers.split(","):
+        for nt in [int(t) for t in args.threads.split(",")]:
+            ld = inet.ImagenetLoader(d, args.batch, True, num_threads=nt, prefetch=3, num_epochs=None,
+                                     workers=workers)
+            next(ld)  # warm-up batch (process workers start here)
+            t0 = time.perf_counter()
+            nb = max(2, args.images // args.batch)
+            for _ in range(nb):
+                next(ld)
+            dt = time.perf_counter() - t0
+            ld.close()
+            print(json.dumps({"what": "loader", "workers": workers, "n": nt, "batch": args.batch,
+                              "img_per_s": round(nb * args.batch / dt, 1), "cpus": os.cpu_count()}), flush=True)
 
 
 if __name__ == "__main__":

@@ -4,7 +4,7 @@ Run under torchrun --nproc-per-node 1 on a GPU box."""
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))  # repo root
 import torch
 import torch.distributed as dist
 

@@ -39,3 +39,32 @@ for p, q in zip(ms, ms[1:]):
 print(f"main-stream gaps: total {sum(g for g, _, _ in gaps) / 1e3:.1f} us over {len(gaps)} gaps")
 for g, p, q in sorted(gaps, reverse=True)[:12]:
     print(f"  {g / 1e3:7.1f} us  after {p}  before {q}")
+
+
+# Overlap accounting: a main-stream gap is only idle GPU time when no other stream runs either.
+def _union(iv):
+    out = []
+    for a, b in sorted(iv):
+        if out and a <= out[-1][1]:
+            out[-1][1] = max(out[-1][1], b)
+        else:
+            out.append([a, b])
+    return out
+
+
+def _covered(a, b, iv):
+    return sum(max(0, min(b, y) - max(a, x)) for x, y in iv)
+
+
+others = _union([(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for s, rs in by.items() if s != main
+                 for r in rs])
+main_iv = _union([(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in ms])
+all_iv = _union(main_iv + others)
+gap_cov = sum(_covered(int(p["End_Timestamp"]), int(q["Start_Timestamp"]), others)
+              for p, q in zip(ms, ms[1:]) if int(q["Start_Timestamp"]) > int(p["End_Timestamp"]))
+both = sum(_covered(a, b, others) for a, b in main_iv)
+idle = (t1 - t0) - sum(b - a for a, b in all_iv)
+print(f"main-stream gaps covered by other streams' kernels: {gap_cov / 1e3:.1f} us "
+      f"(truly idle GPU inside the step: {idle / 1e3:.1f} us)")
+print(f"main and other streams running concurrently: {both / 1e3:.1f} us "
+      f"({both / max(1, sum(b - a for a, b in others)):.0%} of the other streams' busy time)")

@@ -92,6 +92,23 @@ def test_imagenet_loader_batches(tmp_path):
     ld.close()
 
 
+def test_imagenet_loader_process_workers_match_threads(tmp_path):
+    """Spawned decode processes (pixels through named shared memory) give the same batches as
+    the thread pool, and leave no segment behind in /dev/shm."""
+    import glob
+    import os
+    imagenet.write_fake_imagenet(str(tmp_path), shards=2, per_shard=6)
+    got = {}
+    for w in ("thread", "process"):
+        ld = imagenet.ImagenetLoader(str(tmp_path), 4, True, seed=4, num_threads=2, num_epochs=1, workers=w)
+        got[w] = [tuple(np.array(x, copy=True) for x in next(ld)) for _ in range(3)]
+        ld.close()
+    for a, b in zip(got["thread"], got["process"]):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+    assert not glob.glob(f"/dev/shm/{imagenet._SHM_PREFIX}{os.getpid()}_*")
+
+
 def _drain(loader, n):
     out = []
     for _ in range(n):

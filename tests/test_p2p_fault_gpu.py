@@ -16,6 +16,7 @@ handling at all (SyncReplicas stalls forever, resnet_model.py:108-116; SURVEY §
 """
 import os
 import socket
+import sys
 import time
 
 import pytest
@@ -73,12 +74,15 @@ def _worker(rank, mode, port, ck, q, stop):
         save_fn = lambda step, blocking: sess.save(step, blocking)  # noqa: E731
         t0 = time.time()
         err = None
+        print(f"[rank 0] failing phase starts ({mode})", file=sys.stderr, flush=True)
         try:
-            sess.run(feeder, [StopAtStepHook(5)], chief_hooks=[CheckpointHook(0, save_fn)])
+            sess.run(feeder, [StopAtStepHook(4)], chief_hooks=[CheckpointHook(0, save_fn)])
         except RuntimeError as e:
             err = str(e)
         dt = time.time() - t0
+        print(f"[rank 0] run() returned after {dt:.1f} s: {err}", file=sys.stderr, flush=True)
         torch.cuda.synchronize()
+        print("[rank 0] device drained", file=sys.stderr, flush=True)
         same = torch.equal(w0, sess.ex.P.master) and torch.equal(m0, sess.ex.P.momentum)
         later = sorted(f for f in os.listdir(ck) if f.startswith("model.ckpt-") and not f.startswith("model.ckpt-2."))
         q.put((0, (err, dt, same, later, sess.failed)))
@@ -89,7 +93,7 @@ def _worker(rank, mode, port, ck, q, stop):
         os._exit(2)
 
 
-@pytest.mark.timeout(240)
+@pytest.mark.timeout(170)
 @pytest.mark.parametrize("mode", ["withhold", "stall"])
 def test_p2p_peer_failure_skips_update_and_aborts(tmp_path, mode):
     ctx = mp.get_context("spawn")
@@ -102,10 +106,10 @@ def test_p2p_peer_failure_skips_update_and_aborts(tmp_path, mode):
     res = {}
     try:
         while len(res) < 2:
-            r, v = q.get(timeout=200)
+            r, v = q.get(timeout=150)
             res[r] = v
-            if r == 1 and v != "stopped":
-                break  # rank 1 failed during the good steps: report it
+            if isinstance(v, str) and v != "stopped":
+                break  # a rank failed outside the injected fault: the other may be stuck in a collective
     finally:
         stop.set()
         for p in ps:
