@@ -185,6 +185,12 @@ struct DrnConvFwdArgs {
   // x holds the ReLU-masked gradient g, bnb_x the BatchNorm's input.
   const void* bnb_x;
   DrnBnFin bnb_fin;
+  // Split-K (LDS-DMA kernels, ksplit > 1): partial-tile workspace [tiles][ksplit][BP*BC] fp32 and
+  // one zeroed ticket word per output tile (the last arriver re-arms it)
+  float* ks_ws;
+  unsigned* ks_tickets;
+  int32_t ksplit;
+  int32_t pad_ks_;
 };
 
 // dW[K][R][S][C] (+)= sum_{n,p,q} dy[n,p,q,k] * x[n, p*st-pad+r, q*st-pad+s, c]

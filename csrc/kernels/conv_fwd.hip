@@ -655,8 +655,16 @@ __device__ __forceinline__ int glds_swz(int row) {
 // landed g pieces in place (the same one-LDS-round-trip scheme as PRO), zero pieces stay zero.
 // The coefficients come from the BN statistics replicas in the prologue (consumer-side
 // finalize; the first workgroup of the publishing launch writes dgamma / dbeta).
+//
+// KS (split-K, a.ksplit = S > 1): the grid is tiles x S; workgroup (tile, s) runs k-stages
+// [s*T/S, (s+1)*T/S) of its tile, stores its fp32 partial accumulators to a.ks_ws and takes a
+// ticket; the LAST arriver of a tile sums the S partials in split order (fixed order: bitwise
+// reproducible whatever the arrival order) and runs the fused epilogue. No workgroup ever waits
+// on another (no deadlock at any residency); the hand-off is the agent-scope release / acquire
+// pair of the CDNA4 guide (G16). For under-filled grids (e.g. 196 tiles of a 7x7-stage 3x3
+// conv on 256 CUs) it trades 64 KB of partial traffic per extra split for a full chip.
 template <int BP, int BC, int WAVES_P, int NS, int NW = 4, bool PF = true, int BK = 64, bool PRO = false,
-          bool SROW = false, bool BNB = false, int NH = 1>
+          bool SROW = false, bool BNB = false, int NH = 1, bool KS = false, bool IL = false>
 __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a, const void* __restrict__ zero) {
   static_assert(BK == 64 || BK == 32, "k per stage");
   static_assert(!SROW || BK == 64, "row-staged narrow convs: 64-deep stages");
@@ -691,7 +699,11 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   const int C = a.C;
   const int Ktot = a.R * a.S * C;
   const int ntc = (a.K + BC - 1) / BC;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  static_assert(!KS || (!SROW && !BNB), "split-K: plain / fused-BN-prologue inputs");
+  const int ksn = KS ? a.ksplit : 1;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);  // (a tile's splits stay on one XCD)
+  const int bid = KS ? lin / ksn : lin;
+  const int ksi = KS ? lin - bid * ksn : 0;
   const int tc = bid % ntc;
   const int tp = bid / ntc;
   const int m0 = tp * BP;
@@ -735,6 +747,17 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   }
   // wave-uniform k iterator of the next stage to issue: k offset, tap (r, s), channel offset
   int ik = 0, ir = 0, is = 0, ici = 0;
+  int t_beg = 0, t_cnt = 0;  // KS: this split's k-stage range
+  if constexpr (KS) {
+    const int t_all = Ktot / BK;
+    t_beg = (int)((long)ksi * t_all / ksn);
+    t_cnt = (int)((long)(ksi + 1) * t_all / ksn) - t_beg;
+    ik = t_beg * BK;
+    const int tap = ik / C;
+    ici = ik - tap * C;
+    ir = tap / a.S;
+    is = tap - ir * a.S;
+  }
 
   auto issue = [&](int slot) {
     char* st = smem + slot * STAGE;
@@ -787,6 +810,31 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
     kstep_next<BK>(ir, is, ici, a.R, a.S, C);
     ik = (ir * a.S + is) * C + ici;
   };
+  // IL: the same stage issued one LDS-DMA piece at a time (g = 0 .. G-1, A pieces then B pieces
+  // then BNB pieces), interleaved with the MFMAs of the computing stage by the main loop; then
+  // issue_advance() moves the k iterator
+  auto issue_piece = [&](int slot, int g) {
+    char* st = smem + slot * STAGE;
+    if (g < GA) {
+      const void* src = wsrc[g] ? (const void*)(wsrc[g] + ik) : zero;
+      glds16(src, st + (RPG * NW * g + RPG * wave) * ROWB);
+      return;
+    }
+    const int i = (g - GA) % GB;
+    const int h = bh[i] + ir, w = bw[i] + is;
+    const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+    const int off = boff[i] + (ir * a.W + is) * C + ici;
+    if (g < GA + GB) {
+      glds16(ok ? (const void*)(xg + off) : zero, st + (BC + RPG * NW * i + RPG * wave) * ROWB);
+    } else if constexpr (BNB) {
+      const bf16_t* __restrict__ bx = reinterpret_cast<const bf16_t*>(a.bnb_x);
+      glds16(ok ? (const void*)(bx + off) : zero, st + (BC + BP + RPG * NW * i + RPG * wave) * ROWB);
+    }
+  };
+  auto issue_advance = [&]() {
+    kstep_next<BK>(ir, is, ici, a.R, a.S, C);
+    ik = (ir * a.S + is) * C + ici;
+  };
 
   const int wp = wave % WAVES_P;
   const int wc = wave / WAVES_P;
@@ -805,7 +853,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   for (int j = 0; j < MJ; ++j) boffl[j] = (BC + wp * WP + j * 16 + fr) * ROWB;
   const int swz = glds_swz<BK>(fr);  // fragment row groups are 16-aligned: the swizzle bits are fr's
 
-  const int T = SROW ? (C == 4 ? (a.R + 1) / 2 : a.R) : Ktot / BK;
+  const int T = KS ? t_cnt : SROW ? (C == 4 ? (a.R + 1) / 2 : a.R) : Ktot / BK;
   // fused-BN operands: [scale C][shift C] fp32 behind the stages, written AFTER the first
   // pipeline stages are issued (their LDS-DMA latency covers the parameter loads / finalize)
   // (behind the stages actually used: a convolution with fewer k-stages than NS - e.g. a 1x1
@@ -816,6 +864,11 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   static_assert((RPG * NW) % 16 == 0, "piece stride must preserve the swizzle bits");
   const int lcb = lpc ^ glds_swz<BK>(RPG * wave + lrow);
   int xr = 0, xs = 0, xci = 0;  // tap / channel offset of the stage being transformed
+  if constexpr (KS) {
+    xr = ir;
+    xs = is;
+    xci = ici;
+  }
   EpiPre<BP, BC / NH, NT, PF> epre;
   if constexpr (NH == 1)
     epi_prefetch<BP, BC, NT, PF>(a, m0, c0, M, epre);  // residual / BN inputs in flight during the main loop
@@ -925,8 +978,45 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + D < T) issue((t + D) % NS);
     const char* st = smem + (t % NS) * STAGE;
+    if constexpr (IL && !SROW) {
+      // the next stage's LDS-DMA pieces spread between this stage's MFMAs: the DMA issue cost
+      // (~0.1 us per piece per wave) hides under the matrix pipe instead of idling it after
+      // every barrier while all waves issue in lockstep
+      const bool more = t + D < T;
+      const int nslot = (t + D) % NS;
+      constexpr int Q = (BK / 32) * MI * MJ;
+      constexpr int STEP = Q / (G + 1) > 0 ? Q / (G + 1) : 1;
+#pragma unroll
+      for (int kh = 0; kh < BK / 32; ++kh) {
+        const int slot = ((kh * 4 + fk) ^ swz) * 16;
+        bf16x8_t af[MI], bfr[MJ];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) af[i] = *reinterpret_cast<const bf16x8_t*>(st + aoff[i] + slot);
+#pragma unroll
+        for (int j = 0; j < MJ; ++j) bfr[j] = *reinterpret_cast<const bf16x8_t*>(st + boffl[j] + slot);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < MJ; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+            const int q = (kh * MI + i) * MJ + j + 1;
+            if (q % STEP == 0 && q / STEP <= G && more) {
+              __builtin_amdgcn_sched_barrier(0);
+              issue_piece(nslot, q / STEP - 1);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+      }
+      if (Q / STEP < G && more) {  // (fewer MFMAs than pieces: the rest now)
+#pragma unroll
+        for (int g = Q / STEP; g < G; ++g) issue_piece(nslot, g);
+      }
+      if (more) issue_advance();
+      asm volatile("" ::: "memory");
+      continue;
+    }
+    if (t + D < T) issue((t + D) % NS);
 #pragma unroll
     for (int kh = 0; kh < BK / 32; ++kh) {
       const int slot = ((kh * 4 + fk) ^ swz) * 16;
@@ -946,6 +1036,47 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
     asm volatile("" ::: "memory");
   }
   __syncthreads();  // all fragment reads done before the epilogue reuses the LDS
+  if constexpr (KS) {
+    if (ksn > 1) {
+      // publish this split's partial tile (lane-linear: 1 KB per wave-instruction), ticket
+      constexpr int PER = NT * MI * MJ * 4;  // floats per partial tile (= BP * BC)
+      float* ws = a.ks_ws + (size_t)bid * ksn * PER;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < MJ; ++j)
+          *reinterpret_cast<f32x4_t*>(ws + (size_t)ksi * PER + ((i * MJ + j) * NT + tid) * 4) = acc[i][j];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      int* flag = reinterpret_cast<int*>(smem);
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(a.ks_tickets + bid, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = t + 1u == (unsigned)ksn;
+        if (last) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(a.ks_tickets + bid, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+        }
+        *flag = last;
+      }
+      __syncthreads();
+      if (!*flag) return;
+      __syncthreads();  // every wave has read the flag before the epilogue reuses this LDS word
+      // the tile's sum in split order (fixed: bitwise reproducible)
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < MJ; ++j) {
+          f32x4_t sum = f32x4_t{0.f, 0.f, 0.f, 0.f};
+          for (int s = 0; s < ksn; ++s)
+            sum += s == ksi ? acc[i][j]
+                            : *reinterpret_cast<const f32x4_t*>(ws + (size_t)s * PER + ((i * MJ + j) * NT + tid) * 4);
+          acc[i][j] = sum;
+        }
+    }
+  }
 #ifdef DRN_CONV_TRACE
   unsigned long long t_loop = 0;
   if (trace != nullptr) t_loop = drn_realtime();
@@ -981,7 +1112,7 @@ static int cfin_max_blocks() {
 }
 
 template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF, int BK, bool PRO, bool SROW = false, bool BNB = false,
-          int NH = 1>
+          int NH = 1, bool KS = false, bool IL = false>
 static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
   const int T = a->C == 4 ? (a->R + 1) / 2 : a->C == 8 || a->C == 16 ? a->R : (a->R * a->S * a->C) / BK;  // k-stages
                                                           // (SROW: filter rows; packed stem: row pairs)
@@ -990,7 +1121,7 @@ static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t 
   const int LDS = lds_main > BP * BC * 4 / NH ? lds_main : BP * BC * 4 / NH;  // epilogue staging slice
   if (LDS > 160 * 1024) return (int)hipErrorInvalidValue;
   static bool attr_set = false;
-  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS, NW, PF, BK, PRO, SROW, BNB, NH>;
+  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS, NW, PF, BK, PRO, SROW, BNB, NH, KS, IL>;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
@@ -999,7 +1130,9 @@ static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t 
   const int tiles_p = (M + BP - 1) / BP;
   const int tiles_c = (a->K + BC - 1) / BC;
   a->tiles_p = tiles_p;
-  if (PRO && a->in_fin.stats != nullptr && tiles_p * tiles_c > cfin_max_blocks()) {
+  const int ks = KS ? a->ksplit : 1;
+  if (KS && (ks < 2 || T < ks || a->ks_ws == nullptr || a->ks_tickets == nullptr)) return (int)hipErrorInvalidValue;
+  if (PRO && a->in_fin.stats != nullptr && tiles_p * tiles_c * ks > cfin_max_blocks()) {
     // a large grid pays the in-prologue finalize once per workgroup wave: measured slower than
     // one separate finalize launch (ResNet-50 stage 1, 12544 workgroups: +11 us vs ~6 us)
     if (a->in_fin.publish) {
@@ -1008,34 +1141,52 @@ static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t 
     }
     DrnConvFwdArgs b = *a;
     b.in_fin.stats = nullptr;
-    hipLaunchKernelGGL(kern, dim3(tiles_p * tiles_c), dim3(NW * 64), LDS, stream, b, zero);
+    hipLaunchKernelGGL(kern, dim3(tiles_p * tiles_c * ks), dim3(NW * 64), LDS, stream, b, zero);
     return (int)hipGetLastError();
   }
-  hipLaunchKernelGGL(kern, dim3(tiles_p * tiles_c), dim3(NW * 64), LDS, stream, *a, zero);
+  hipLaunchKernelGGL(kern, dim3(tiles_p * tiles_c * ks), dim3(NW * 64), LDS, stream, *a, zero);
   return (int)hipGetLastError();
 }
 
-template <int BP, int BC, int WAVES_P, int NS, int NW, int BK>
+template <int BP, int BC, int WAVES_P, int NS, int NW, int BK, bool IL>
 static int launch_conv_glds_nh1(DrnConvFwdArgs* a, const void* zero, hipStream_t stream);
 
+// split-K launch (a->ksplit > 1): plain / fused-BN-prologue inputs only
+template <int BP, int BC, int WAVES_P, int NS, int NW, int BK, int NH, bool IL>
+static int launch_conv_glds_ks(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
+  if (a->C == 4 || a->C == 8 || a->C == 16 || a->C % BK || a->bnb_x != nullptr) return (int)hipErrorInvalidValue;
+  // epilogue operands: prefetched by the (NH == 1) kernels that keep them in registers
+  constexpr bool PFOK = NH == 1;
+  const bool pf = PFOK && (a->residual != nullptr || a->bn_x != nullptr);
+  if (a->in_scale != nullptr)
+    return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, PFOK, BK, true, false, false, NH, true, IL>(a, zero, stream)
+              : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, true, false, false, NH, true, IL>(a, zero, stream);
+  return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, PFOK, BK, false, false, false, NH, true, IL>(a, zero, stream)
+            : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false, false, false, NH, true, IL>(a, zero, stream);
+}
+
 // epilogue operands (residual / BN-backward input) are prefetched only when present
-template <int BP, int BC, int WAVES_P, int NS, int NW = 4, int BK = 64, int NH = 1>
+template <int BP, int BC, int WAVES_P, int NS, int NW = 4, int BK = 64, int NH = 1, bool IL = false, bool KSOK = false>
 static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
+  if (a->ksplit > 1) {
+    if constexpr (KSOK) return launch_conv_glds_ks<BP, BC, WAVES_P, NS, NW, BK, NH, IL>(a, zero, stream);
+    return (int)hipErrorInvalidValue;
+  }
   if constexpr (NH > 1) {  // big tiles: plain / fused-BN-prologue input, sliced epilogue, no prefetch
     if (a->C == 4 || a->C == 8 || a->C == 16 || a->C % BK || a->bnb_x != nullptr) return (int)hipErrorInvalidValue;
     if (a->in_scale != nullptr)
-      return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, true, false, false, NH>(a, zero, stream);
-    return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false, false, false, NH>(a, zero, stream);
+      return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, true, false, false, NH, false, IL>(a, zero, stream);
+    return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false, false, false, NH, false, IL>(a, zero, stream);
   } else {
-    return launch_conv_glds_nh1<BP, BC, WAVES_P, NS, NW, BK>(a, zero, stream);
+    return launch_conv_glds_nh1<BP, BC, WAVES_P, NS, NW, BK, IL>(a, zero, stream);
   }
 }
 
-template <int BP, int BC, int WAVES_P, int NS, int NW, int BK>
+template <int BP, int BC, int WAVES_P, int NS, int NW, int BK, bool IL>
 static int launch_conv_glds_nh1(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
   const bool pf = a->residual != nullptr || a->bn_x != nullptr;
   if (a->C == 4 || a->C == 8 || a->C == 16) {  // row-staged narrow conv (the stem, the CIFAR first stage)
-    if constexpr (BK == 64) {
+    if constexpr (BK == 64 && !IL) {
       if (a->S * a->C > (a->C == 4 ? 32 : 64)) return (int)hipErrorInvalidValue;
       if (a->C == 4 && (a->S % 2 || a->in_scale != nullptr)) return (int)hipErrorInvalidValue;
       if (a->in_scale != nullptr)
@@ -1049,60 +1200,68 @@ static int launch_conv_glds_nh1(DrnConvFwdArgs* a, const void* zero, hipStream_t
   if (a->C % BK) return (int)hipErrorInvalidValue;
   if (a->bnb_x != nullptr) {  // fused BN-backward input (data gradients): 64-deep stages only
     if constexpr (BK == 64)
-      return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, false, false, true>(a, zero, stream)
-                : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false, false, true>(a, zero, stream);
+      return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, false, false, true, 1, false, IL>(a, zero, stream)
+                : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false, false, true, 1, false, IL>(a, zero, stream);
     return (int)hipErrorInvalidValue;
   }
   if (a->in_scale != nullptr)
-    return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, true>(a, zero, stream)
-              : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, true>(a, zero, stream);
-  return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, false>(a, zero, stream)
-            : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false>(a, zero, stream);
+    return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, true, false, false, 1, false, IL>(a, zero, stream)
+              : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, true, false, false, 1, false, IL>(a, zero, stream);
+  return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, false, false, false, 1, false, IL>(a, zero, stream)
+            : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false, false, false, 1, false, IL>(a, zero, stream);
 }
 
 // Tile configurations of the LDS-DMA kernel (index = DRN conv config id, also used by the
-// host-side autotuner): {BP, BC, WAVES_P, NS, NW, BK, NH}. 25-30 are the 8-wave big tiles with
-// 32-deep stages and 3-4 stages in flight (one workgroup per CU, ~96 KB of LDS-DMA in flight):
-// a 128 x 128 tile needs 64 B per MFMA cycle from L2 -- the per-CU L2 read rate -- so it can
-// never keep the matrix pipe busy; 256 x 256 needs half that, 256 x 128 three quarters.
-#define DRN_GLDS_CONFIGS(X)      \
-  X(0, 128, 128, 2, 2, 4, 64, 1)  \
-  X(1, 128, 128, 2, 3, 4, 64, 1)  \
-  X(2, 128, 128, 2, 4, 4, 64, 1)  \
-  X(3, 256, 64, 4, 2, 4, 64, 1)   \
-  X(4, 256, 64, 4, 3, 4, 64, 1)   \
-  X(5, 128, 64, 2, 3, 4, 64, 1)   \
-  X(6, 64, 128, 1, 3, 4, 64, 1)   \
-  X(7, 64, 64, 2, 4, 4, 64, 1)    \
-  X(8, 256, 128, 4, 2, 8, 64, 1)  \
-  X(9, 256, 128, 4, 3, 8, 64, 1)  \
-  X(10, 128, 256, 2, 2, 8, 64, 1) \
-  X(11, 128, 256, 2, 3, 8, 64, 1) \
-  X(12, 128, 64, 2, 2, 4, 64, 1)  \
-  X(13, 64, 128, 1, 2, 4, 64, 1)  \
-  X(14, 64, 64, 2, 2, 4, 64, 1)   \
-  X(15, 64, 256, 1, 2, 4, 64, 1)  \
-  X(16, 32, 128, 1, 2, 4, 64, 1)  \
-  X(17, 128, 128, 2, 4, 4, 32, 1) \
-  X(18, 64, 128, 1, 4, 4, 32, 1)  \
-  X(19, 128, 64, 2, 4, 4, 32, 1)  \
-  X(20, 128, 128, 2, 3, 4, 32, 1) \
-  X(21, 64, 128, 1, 3, 4, 32, 1)  \
-  X(22, 256, 64, 4, 4, 4, 32, 1)  \
-  X(23, 256, 32, 4, 2, 4, 64, 1)  \
-  X(24, 128, 32, 4, 3, 4, 64, 1)  \
-  X(25, 256, 256, 4, 4, 8, 32, 2) \
-  X(26, 256, 256, 4, 2, 8, 64, 2) \
-  X(27, 256, 128, 4, 5, 8, 32, 1) \
-  X(28, 128, 256, 2, 5, 8, 32, 1) \
-  X(29, 256, 256, 2, 4, 8, 32, 2) \
-  X(30, 256, 128, 2, 4, 8, 32, 1)
+// host-side autotuner): {BP, BC, WAVES_P, NS, NW, BK, NH, IL, KS}. 25-30: 8-wave big tiles with
+// 32-deep stages and 3-4 stages in flight (one workgroup per CU): a 128 x 128 tile needs 64 B per
+// MFMA cycle from L2 -- the per-CU L2 read rate -- 256 x 256 half that. IL = the next stage's
+// LDS-DMA pieces interleaved with the MFMAs (31-37 = IL twins of the most used configs).
+// KS = split-K capable (DrnConvFwdArgs::ksplit > 1, last-arriver epilogue).
+#define DRN_GLDS_CONFIGS(X)                 \
+  X(0, 128, 128, 2, 2, 4, 64, 1, false, true)  \
+  X(1, 128, 128, 2, 3, 4, 64, 1, false, false) \
+  X(2, 128, 128, 2, 4, 4, 64, 1, false, false) \
+  X(3, 256, 64, 4, 2, 4, 64, 1, false, false)  \
+  X(4, 256, 64, 4, 3, 4, 64, 1, false, false)  \
+  X(5, 128, 64, 2, 3, 4, 64, 1, false, false)  \
+  X(6, 64, 128, 1, 3, 4, 64, 1, false, false)  \
+  X(7, 64, 64, 2, 4, 4, 64, 1, false, false)   \
+  X(8, 256, 128, 4, 2, 8, 64, 1, false, false) \
+  X(9, 256, 128, 4, 3, 8, 64, 1, false, false) \
+  X(10, 128, 256, 2, 2, 8, 64, 1, false, false) \
+  X(11, 128, 256, 2, 3, 8, 64, 1, false, false) \
+  X(12, 128, 64, 2, 2, 4, 64, 1, false, false) \
+  X(13, 64, 128, 1, 2, 4, 64, 1, false, true)  \
+  X(14, 64, 64, 2, 2, 4, 64, 1, false, false)  \
+  X(15, 64, 256, 1, 2, 4, 64, 1, false, false) \
+  X(16, 32, 128, 1, 2, 4, 64, 1, false, false) \
+  X(17, 128, 128, 2, 4, 4, 32, 1, false, false) \
+  X(18, 64, 128, 1, 4, 4, 32, 1, false, false) \
+  X(19, 128, 64, 2, 4, 4, 32, 1, false, false) \
+  X(20, 128, 128, 2, 3, 4, 32, 1, false, false) \
+  X(21, 64, 128, 1, 3, 4, 32, 1, false, false) \
+  X(22, 256, 64, 4, 4, 4, 32, 1, false, false) \
+  X(23, 256, 32, 4, 2, 4, 64, 1, false, false) \
+  X(24, 128, 32, 4, 3, 4, 64, 1, false, false) \
+  X(25, 256, 256, 4, 4, 8, 32, 2, false, true) \
+  X(26, 256, 256, 4, 2, 8, 64, 2, false, false) \
+  X(27, 256, 128, 4, 5, 8, 32, 1, false, false) \
+  X(28, 128, 256, 2, 5, 8, 32, 1, false, false) \
+  X(29, 256, 256, 2, 4, 8, 32, 2, false, false) \
+  X(30, 256, 128, 2, 4, 8, 32, 1, false, false) \
+  X(31, 128, 128, 2, 2, 4, 64, 1, true, true)   \
+  X(32, 64, 128, 1, 2, 4, 64, 1, true, true)    \
+  X(33, 256, 256, 4, 4, 8, 32, 2, true, true)   \
+  X(34, 256, 128, 4, 2, 8, 64, 1, true, false)  \
+  X(35, 64, 256, 1, 2, 4, 64, 1, true, false)   \
+  X(36, 128, 64, 2, 4, 4, 32, 1, true, false)   \
+  X(37, 64, 128, 1, 3, 4, 32, 1, true, false)
 
 static int launch_glds_cfg(int cfg, DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
   switch (cfg) {
-#define DRN_X(id, bp, bc, wpv, ns, nw, bk, nh) \
-  case id:                                     \
-    return launch_conv_glds<bp, bc, wpv, ns, nw, bk, nh>(a, zero, s);
+#define DRN_X(id, bp, bc, wpv, ns, nw, bk, nh, il, ks) \
+  case id:                                             \
+    return launch_conv_glds<bp, bc, wpv, ns, nw, bk, nh, il, ks>(a, zero, s);
     DRN_GLDS_CONFIGS(DRN_X)
 #undef DRN_X
     default:
@@ -1112,9 +1271,21 @@ static int launch_glds_cfg(int cfg, DrnConvFwdArgs* a, const void* zero, hipStre
 
 static int glds_cfg_bp(int cfg) {
   switch (cfg) {
-#define DRN_X(id, bp, bc, wpv, ns, nw, bk, nh) \
-  case id:                                     \
+#define DRN_X(id, bp, bc, wpv, ns, nw, bk, nh, il, ks) \
+  case id:                                             \
     return bp;
+    DRN_GLDS_CONFIGS(DRN_X)
+#undef DRN_X
+    default:
+      return 0;
+  }
+}
+
+static int glds_cfg_bc(int cfg) {
+  switch (cfg) {
+#define DRN_X(id, bp, bc, wpv, ns, nw, bk, nh, il, ks) \
+  case id:                                             \
+    return bc;
     DRN_GLDS_CONFIGS(DRN_X)
 #undef DRN_X
     default:
@@ -1175,7 +1346,7 @@ DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s);
 DRN_API int drn_conv_mt(int cfg, DrnConvFwdArgs* a, const void* zero, hipStream_t s);
 DRN_API int drn_conv_mt_num_cfgs();
 DRN_API int drn_conv_mt_ok(const DrnConvFwdArgs* a);
-#define DRN_GLDS_NCFG 31
+#define DRN_GLDS_NCFG 38
 
 // Whether the LDS-DMA kernel family supports this convolution.
 DRN_API int drn_conv_glds_ok(const DrnConvFwdArgs* a) {
@@ -1201,6 +1372,8 @@ DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
   if (a->in_fin.stats != nullptr &&
       (a->in_scale == nullptr || a->in_fin.C != a->C || a->in_fin.G < 1 || a->in_fin.G > DRN_BN_FIN_GMAX))
     return (int)hipErrorInvalidValue;
+  if (a->ksplit > 1 && (a->cfg < 0 || a->cfg >= DRN_GLDS_NCFG || !drn_conv_glds_ok(a) || zero == nullptr))
+    return (int)hipErrorInvalidValue;  // split-K: explicit split-capable LDS-DMA configurations only
   if (a->cfg >= DRN_GLDS_NCFG && a->cfg != 100) return drn_conv_mt(a->cfg - DRN_GLDS_NCFG, a, zero, s);
   if (a->bnb_x != nullptr && (!drn_conv_glds_ok(a) || zero == nullptr || a->cfg == 100))
     return (int)hipErrorInvalidValue;  // the BN-backward input transform exists on the LDS-DMA path only
@@ -1226,6 +1399,7 @@ DRN_API int drn_conv_trace_set(unsigned long long* buf) {
 #endif
 
 DRN_API int drn_conv_glds_cfg_bp(int cfg) { return drn::glds_cfg_bp(cfg); }
+DRN_API int drn_conv_glds_cfg_bc(int cfg) { return drn::glds_cfg_bc(cfg); }
 DRN_API int drn_conv_glds_num_cfgs() { return DRN_GLDS_NCFG + drn_conv_mt_num_cfgs(); }
 DRN_API int drn_conv_glds_default_cfg(const DrnConvFwdArgs* a) { return drn::glds_default_cfg(a); }
 

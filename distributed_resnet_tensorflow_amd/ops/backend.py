@@ -226,7 +226,12 @@ class HipBackend(_Common):
         # 4 KiB of device zeros: the padding source of the LDS-DMA conv loader
         self.zero_page = torch.zeros(1024, dtype=torch.float32, device=self.device)
         # conv kernel config per geometry key (set by the autotuner; -1 = library default)
-        self.conv_cfg: dict = {}
+        self.conv_cfg: dict = {}          # geometry key -> (config id, split-K factor)
+        # split-K conv launches (DrnConvFwdArgs.ksplit): fp32 partial-tile workspace (grown before
+        # any graph capture: the autotuner sizes it) and one ticket word per output tile
+        self.ks_ws = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.ks_tickets = torch.zeros(1 << 16, dtype=torch.int32, device=self.device)
+        self.KS_FACTORS = tuple(int(v) for v in os.environ.get("DRN_CONV_KSPLIT", "2,3,4").split(",") if v)
         forced = os.environ.get("DRN_CONV_CFG")
         self.forced_cfg = int(forced) if forced not in (None, "") else None
         self.autotune = os.environ.get("DRN_AUTOTUNE", "1") == "1"
@@ -299,8 +304,28 @@ class HipBackend(_Common):
             assert bx.shape == x.shape and in_bn is None and bf.C == C
             a.bnb_x = bx.data_ptr()
             a.bnb_fin = bf.struct()
-        a.cfg = self.forced_cfg if self.forced_cfg is not None else self.conv_cfg.get(self.conv_key(a), -1)
+        cfg, ks = (self.forced_cfg, 1) if self.forced_cfg is not None else self.conv_cfg.get(self.conv_key(a), (-1, 1))
+        a.cfg = cfg
+        self._set_ksplit(a, ks)
         return a
+
+    def _ks_need(self, a, ks: int) -> int:
+        """fp32 elements of split-K workspace a launch of config a.cfg with factor ks needs."""
+        bp, bc = self.L.drn_conv_glds_cfg_bp(a.cfg), self.L.drn_conv_glds_cfg_bc(a.cfg)
+        if bp <= 0 or bc <= 0:
+            return 0
+        M = a.N * a.P * a.Q
+        return ((M + bp - 1) // bp) * ((a.K + bc - 1) // bc) * ks * bp * bc
+
+    def _set_ksplit(self, a, ks: int):
+        a.ksplit = int(ks) if ks and ks > 1 else 0
+        if a.ksplit > 1:
+            need = self._ks_need(a, a.ksplit)
+            if need > self.ks_ws.numel():
+                if torch.cuda.is_current_stream_capturing():
+                    raise RuntimeError("split-K workspace must be sized before graph capture (autotune first)")
+                self.ks_ws = torch.empty(need, dtype=torch.float32, device=self.device)
+            a.ks_ws, a.ks_tickets = self.ks_ws.data_ptr(), self.ks_tickets.data_ptr()
 
     @staticmethod
     def conv_key(a) -> tuple:
@@ -313,7 +338,9 @@ class HipBackend(_Common):
             key = self.conv_key(a)
             if key not in self.conv_cfg and not torch.cuda.is_current_stream_capturing():
                 self.conv_cfg[key] = self._tune_conv(a, key)
-            a.cfg = self.conv_cfg.get(key, -1)
+            cfg, ks = self.conv_cfg.get(key, (-1, 1))
+            a.cfg = cfg
+            self._set_ksplit(a, ks)
         _lib.check(self.L.drn_conv_fwd2(ctypes.byref(a), self.zero_page.data_ptr(), self.stream()), "drn_conv_fwd")
 
     def _tune_conv(self, a, key, iters: int = 5) -> int:
@@ -322,7 +349,7 @@ class HipBackend(_Common):
         scratch outputs / statistics so no live buffer is modified. Every configuration
         accumulates each output in the same k order, so the choice does not change numerics."""
         if not self.L.drn_conv_glds_ok(ctypes.byref(a)):
-            return 100
+            return (100, 1)
         N, K = a.N, a.K
         oh = a.out_H if a.out_stride else a.P
         ow = a.out_W if a.out_stride else a.Q
@@ -343,8 +370,12 @@ class HipBackend(_Common):
         cands = os.environ.get("DRN_CONV_CANDS")
         cands = [int(c) for c in cands.split(",")] if cands else [100] + list(range(self.L.drn_conv_glds_num_cfgs()))
 
-        def time_cfg(cfg, n):
-            t.cfg = cfg
+        def setk(c):
+            t.cfg, ks = c
+            self._set_ksplit(t, ks)
+
+        def time_cfg(c, n):
+            setk(c)
             _lib.check(self.L.drn_conv_fwd2(ctypes.byref(t), self.zero_page.data_ptr(), s), "drn_conv_fwd")
             ev0.record()
             for _ in range(n):
@@ -353,21 +384,32 @@ class HipBackend(_Common):
             ev1.synchronize()
             return ev0.elapsed_time(ev1) / n
 
+        # candidates: (config, split-K factor); split-K only where the grid leaves CUs idle
+        M = a.N * a.P * a.Q
+        pairs = []
+        for cfg in cands:
+            pairs.append((cfg, 1))
+            bp = self.L.drn_conv_glds_cfg_bp(cfg) if 0 <= cfg < 1000 else 0
+            bc = self.L.drn_conv_glds_cfg_bc(cfg) if 0 <= cfg < 1000 else 0
+            if bp > 0 and bc > 0 and a.out_stride == 0:
+                tiles = ((M + bp - 1) // bp) * ((a.K + bc - 1) // bc)
+                if tiles < 512:
+                    pairs += [(cfg, k) for k in self.KS_FACTORS if k > 1]
         # pass 1: every applicable configuration, short; pass 2: the 4 fastest re-timed twice,
         # interleaved, keeping each one's best (single short timings picked outliers: clock
         # ramps and neighbours' cache state moved the choice by >10 %)
         first = []
-        for cfg in cands:
-            t.cfg = cfg
+        for c in pairs:
+            setk(c)
             if self.L.drn_conv_fwd2(ctypes.byref(t), self.zero_page.data_ptr(), s) != 0:
                 continue  # configuration not applicable to this geometry (e.g. C % 64 != 0)
-            first.append((time_cfg(cfg, iters), cfg))
+            first.append((time_cfg(c, iters), c))
         first.sort()
-        top = {cfg: ms for ms, cfg in first[:4 if os.environ.get("DRN_TUNE_2PASS", "1") == "1" else 1]}
+        top = {c: ms for ms, c in first[:4 if os.environ.get("DRN_TUNE_2PASS", "1") == "1" else 1]}
         for _ in range(2 if len(top) > 1 else 0):
-            for cfg in list(top):
-                top[cfg] = min(top[cfg], time_cfg(cfg, 2 * iters))
-        best, best_t = min(top.items(), key=lambda kv: kv[1]) if top else (100, 0.0)
+            for c in list(top):
+                top[c] = min(top[c], time_cfg(c, 2 * iters))
+        best, best_t = min(top.items(), key=lambda kv: kv[1]) if top else ((100, 1), 0.0)
         self.tune_log.append((key, best, round(best_t * 1e3, 1)))
         return best
 

@@ -165,6 +165,7 @@ def build_variant(out_dir: str, extra: list[str]) -> Path:
     (the source-stamp check is skipped for an explicit library)."""
     out = Path(out_dir).resolve()
     obj_dir = REPO / "build" / ("variant_" + out.name)  # objects stay out of the shipped tree
+    out.mkdir(parents=True, exist_ok=True)
     obj_dir.mkdir(parents=True, exist_ok=True)
     srcs = sources()
     with cf.ThreadPoolExecutor(max_workers=min(len(srcs), 8)) as ex:

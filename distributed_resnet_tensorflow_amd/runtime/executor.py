@@ -103,6 +103,28 @@ class BlockPlan:
     grad_lo: int                    # lowest flat grad offset written by this block
 
 
+def _cu_masked_stream(device, n_cus: int):
+    """A HIP stream whose kernels may only occupy n_cus of the GPU's CUs (hipExtStreamCreateWithCUMask,
+    CUs taken evenly over the whole index range so every XCD contributes): the weight-gradient side
+    stream then leaves the rest of the chip free for the critical-path data gradients instead of
+    holding every CU slot with long-lived blocks (DRN_SIDE_CUS; eager steps -- a captured graph does
+    not keep a stream's CU mask)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
+    total = torch.cuda.get_device_properties(device).multi_processor_count
+    n_cus = max(1, min(n_cus, total))
+    words = (ctypes.c_uint32 * ((total + 31) // 32))()
+    for j in range(n_cus):
+        cu = (j * total) // n_cus
+        words[cu // 32] |= 1 << (cu % 32)
+    st = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(len(words)), words)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+    return torch.cuda.ExternalStream(st.value, device=device)
+
+
 class Executor:
     def __init__(self, spec: NetSpec, batch: int, backend, device, seed: int = 0,
                  weight_decay: float = 2e-4, momentum: float = 0.9, params: ParamStore | None = None,
@@ -157,8 +179,10 @@ class Executor:
         # weight gradients on a second HIP stream (DRN_WGRAD_STREAM=1): every wgrad (+ its split-K
         # reduction) only feeds the optimizer, so it runs concurrently with the data-gradient /
         # BN-backward chain of the critical path; events guard the gradient buffers it reads
-        self.side = torch.cuda.Stream(self.device) if (self.is_hip and
-                                                       os.environ.get("DRN_WGRAD_STREAM", "1") == "1") else None
+        self.side = None
+        if self.is_hip and os.environ.get("DRN_WGRAD_STREAM", "1") == "1":
+            cus = int(os.environ.get("DRN_SIDE_CUS", "0"))
+            self.side = _cu_masked_stream(self.device, cus) if cus > 0 else torch.cuda.Stream(self.device)
         self._pending = {}
         # BN-apply+ReLU either fused into every consuming conv's load prologue (recomputed by the
         # forward conv, the projection conv and both weight-gradient convs; the LDS-DMA kernels

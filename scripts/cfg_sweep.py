@@ -41,10 +41,13 @@ if "stats" in flags:
     kw["stats"] = torch.zeros(8, 2, K, device="cuda")
 out = []
 for cfg in [100] + list(range(be.L.drn_conv_glds_num_cfgs())):
-    a = be.conv_args(x, w, y, g, **kw)
-    a.cfg = cfg
-    if be.L.drn_conv_fwd2(ctypes.byref(a), be.zero_page.data_ptr(), be.stream()) != 0:
-        continue
-    out.append((timeit(lambda: be.L.drn_conv_fwd2(ctypes.byref(a), be.zero_page.data_ptr(), be.stream())), cfg))
+    for ks in (1, 2, 3, 4):  # split-K factors (only the split-capable configurations accept ks > 1)
+        a = be.conv_args(x, w, y, g, **kw)
+        a.cfg = cfg
+        be._set_ksplit(a, ks)
+        if be.L.drn_conv_fwd2(ctypes.byref(a), be.zero_page.data_ptr(), be.stream()) != 0:
+            continue
+        t = timeit(lambda: be.L.drn_conv_fwd2(ctypes.byref(a), be.zero_page.data_ptr(), be.stream()))
+        out.append((t, f"{cfg}" if ks == 1 else f"{cfg}/k{ks}"))
 out.sort()
-print(f"N{N} H{H} C{C} K{K} R{R} s{st} {sorted(flags)}: " + " ".join(f"{c}:{t:.1f}" for t, c in out[:12]), flush=True)
+print(f"N{N} H{H} C{C} K{K} R{R} s{st} {sorted(flags)}: " + " ".join(f"{c}:{t:.1f}" for t, c in out[:14]), flush=True)

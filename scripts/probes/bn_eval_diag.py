@@ -31,7 +31,7 @@ def main():
     import_state(ex, Saver.restore(latest_checkpoint(log_root)))
     import glob
     recs = cifar_data.CifarRecords(sorted(glob.glob(pattern)))
-    nb = max(1, len(recs) // 100)
+    nb = max(1, recs.n // 100)
 
     def batches():
         ld = cifar_data.CifarLoader(recs, 100, False, pin=True, pin_device=torch.device("cuda"))

@@ -1,4 +1,4 @@
-"""Multi-tile LDS-DMA conv family (csrc/kernels/conv_mt.hip, config ids 31..) vs the fp32
+"""Multi-tile LDS-DMA conv family (csrc/kernels/conv_mt.hip, config ids 38..) vs the fp32
 reference: every configuration x epilogue variant (residual, forward BN statistics, fused
 BN-backward reduction, strided output map) x fused input-BN prologue, on geometries with
 several tiles per workgroup, partial pixel / channel tiles and padding."""
@@ -11,7 +11,7 @@ from distributed_resnet_tensorflow_amd.ops.backend import ConvGeom, OutMap
 
 pytestmark = pytest.mark.gpu
 
-MT0 = 31  # first multi-tile config id (after the 31 one-tile LDS-DMA configurations)
+MT0 = 38  # first multi-tile config id (after the 38 one-tile LDS-DMA configurations)
 
 
 def rel(a, b):

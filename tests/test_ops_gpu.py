@@ -89,9 +89,11 @@ GLDS_CASES = [
 ]
 
 
-N_GLDS = 31                              # one-tile LDS-DMA configurations (DRN_GLDS_NCFG)
-BK32 = set(range(17, 23)) | {25, 27, 28, 29, 30}  # 32-deep stages: C % 32 == 0 suffices
-BIG = set(range(25, 31))                 # 8-wave big tiles: no row-staged narrow inputs
+N_GLDS = 38                              # one-tile LDS-DMA configurations (DRN_GLDS_NCFG)
+BK32 = set(range(17, 23)) | {25, 27, 28, 29, 30, 33, 36, 37}  # 32-deep stages: C % 32 == 0 suffices
+BIG = set(range(25, 31)) | {33, 34}      # 8-wave big tiles: no row-staged narrow inputs
+IL = set(range(31, 38))                  # interleaved-DMA twins: no row-staged narrow inputs
+KS = [0, 13, 25, 31, 32, 33]             # split-K capable
 
 
 @pytest.mark.parametrize("case", GLDS_CASES)
@@ -119,7 +121,7 @@ def test_conv_fwd_glds_configs(hip, ref, case, cfg, pro):
     assert hip.L.drn_conv_glds_ok(a) == 1 and a.stats_rep == 3
     a.cfg = cfg
     narrow = C in (8, 16)                # row-staged: the 64-deep-stage configurations only
-    if (C % 64 and not narrow and cfg not in BK32) or (narrow and (cfg in BK32 or cfg in BIG)):
+    if (C % 64 and not narrow and cfg not in BK32) or (narrow and (cfg in BK32 or cfg in BIG or cfg in IL)):
         assert hip.L.drn_conv_fwd2(ctypes.byref(a), hip.zero_page.data_ptr(), hip.stream()) != 0
         return
     hip.launch_conv(a)
@@ -128,6 +130,54 @@ def test_conv_fwd_glds_configs(hip, ref, case, cfg, pro):
     s_hip = st.sum(0).view(-1).cpu()
     assert rel(s_hip[:K], st_ref[:K]) < 2e-2
     assert rel(s_hip[K:], st_ref[K:]) < 2e-2
+
+
+SPLITK_CASES = [
+    # N, H, W, C, K, R, stride, pad
+    (2, 9, 9, 64, 128, 3, 1, 1),       # partial pixel tiles, 9 taps
+    (1, 7, 7, 256, 72, 3, 1, 1),       # K % BC != 0, uneven stage split
+    (3, 8, 8, 128, 256, 1, 1, 0),      # 1x1: 2 / 4 stages split
+]
+
+
+@pytest.mark.parametrize("case", SPLITK_CASES)
+@pytest.mark.parametrize("cfg", KS)
+@pytest.mark.parametrize("ks", [2, 3])
+def test_conv_fwd_splitk(hip, ref, case, cfg, ks):
+    """Split-K launches (partial tiles + last-arriver epilogue) vs the fp32 reference, with the
+    fused BN prologue, residual add and BN statistics, and bitwise equal across two launches
+    (the partials are summed in split order, whatever the arrival order)."""
+    N, H, W, C, K, R, s, p = case
+    torch.manual_seed(30 + ks)
+    P = out_size(H, R, s, p)
+    x = bf(torch.randn(N, H, W, C))
+    w = bf(torch.randn(K, R, R, C) * (2.0 / (R * R * C)) ** 0.5)
+    res = bf(torch.randn(N, P, P, K))
+    g = ConvGeom(stride=s, pad_h=p, pad_w=p)
+    in_bn = (torch.rand(C) + 0.5, torch.randn(C) * 0.5)
+    y_ref = torch.zeros(N, P, P, K)
+    st_ref = torch.zeros(2 * K)
+    ref.conv_fwd(x.float(), w.float(), y_ref, g, in_bn=in_bn, residual=res.float(), stats=st_ref)
+    outs = []
+    for _ in range(2):
+        y = torch.zeros(N, P, P, K, dtype=torch.bfloat16, device="cuda")
+        st = torch.zeros(3, 2, K, device="cuda")
+        a = hip.conv_args(x.cuda(), w.cuda(), y, g, residual=res.cuda(), stats=st,
+                          in_bn=(in_bn[0].cuda(), in_bn[1].cuda()))
+        a.cfg = cfg
+        hip._set_ksplit(a, ks)
+        rc = hip.L.drn_conv_fwd2(ctypes.byref(a), hip.zero_page.data_ptr(), hip.stream())
+        if rc != 0:
+            assert R * R * C // (32 if cfg in BK32 else 64) < ks, (cfg, ks)  # fewer stages than splits
+            return
+        torch.cuda.synchronize()
+        assert rel(y, y_ref) < 1e-2, (cfg, ks)
+        s_hip = st.sum(0).view(-1).cpu()
+        assert rel(s_hip[:K], st_ref[:K]) < 2e-2
+        assert rel(s_hip[K:], st_ref[K:]) < 2e-2
+        outs.append(y.clone())
+    assert torch.equal(outs[0], outs[1])
+    assert int(hip.ks_tickets.abs().sum()) == 0  # every ticket re-armed by its last arriver
 
 
 def test_conv_glds_out_map(hip, ref):
