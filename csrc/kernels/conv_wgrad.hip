@@ -349,7 +349,11 @@ __device__ __forceinline__ void lgkm_fence(s16x4v (&a)[MI][2], s16x4v (&b)[MJ][2
 // lane rewrites its own landed dY pieces as A*g + B*x + D (its 8 channels are fixed for the
 // kernel, so the coefficients live in registers; they are finalized once per workgroup from the
 // backward statistics); pieces past the split / the channel range stay zero.
-template <int BKK, int BCO, int NS, int BP = 64, bool PRO = false, bool BNB = false>
+//
+// IL: the next stage's LDS-DMA pieces are issued one at a time between this stage's MFMAs
+// (instead of all right after the barrier, where every wave issues in lockstep and the matrix
+// pipe idles for the DMA issue time).
+template <int BKK, int BCO, int NS, int BP = 64, bool PRO = false, bool BNB = false, bool IL = false>
 __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a, const void* __restrict__ zero) {
   static_assert(BP == 32 || BP == 64, "pixels per stage");
   constexpr int KS = BP / 32;  // 32-deep MFMA k-slices per stage
@@ -524,6 +528,50 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
     }
   };
 
+  // one piece of issue(): g < IA: patch piece g (and its pixel-state advance); then the dY
+  // pieces, then the BatchNorm-input pieces
+  auto issue_piece = [&](int slot, int mstep, int gp) {
+    char* st = smem + slot * STAGE;
+    if (gp < IA) {
+      const int i = gp;
+      const int r0 = RIA * (wave + 4 * i);
+      const int h = __mul24(ap[i], a.stride) + roff;
+      const int w = __mul24(aq[i], a.stride) + soff;
+      const bool ok = kvalid && am[i] < mend && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+      const uint32_t off = (uint32_t)(__mul24(an[i], HWC) + __mul24(h, WC) + __mul24(w, a.C) + ci);
+      if constexpr (PRO) {
+        const uint32_t bit = 1u << (slot * IA + i);
+        okm = ok ? (okm | bit) : (okm & ~bit);
+      }
+      __builtin_amdgcn_global_load_lds((wg_gbl_void*)(ok ? (const void*)(xg + off) : zero),
+                                       (wg_lds_void*)(st + r0 * WA), 16, 0, 0);
+      am[i] += BP;
+      aq[i] += dq;
+      ap[i] += dp;
+      if (aq[i] >= a.Q) {
+        aq[i] -= a.Q;
+        ++ap[i];
+      }
+      while (ap[i] >= a.P) {
+        ap[i] -= a.P;
+        ++an[i];
+      }
+      return;
+    }
+    const int i = (gp - IA) % IB;
+    const int r0 = RIB * (wave + 4 * i);
+    const int m = mstep + r0 + brow;
+    const bool ok = cvalid && m < mend;
+    if (gp < IA + IB) {
+      __builtin_amdgcn_global_load_lds((wg_gbl_void*)(ok ? (const void*)(dyg + (uint32_t)__mul24(m, a.K)) : zero),
+                                       (wg_lds_void*)(st + A_BYTES + r0 * WB), 16, 0, 0);
+    } else if constexpr (BNB) {
+      __builtin_amdgcn_global_load_lds((wg_gbl_void*)(ok ? (const void*)(bxg + (uint32_t)__mul24(m, a.K)) : zero),
+                                       (wg_lds_void*)(st + A_BYTES + BP * WB + r0 * WB), 16, 0, 0);
+    }
+  };
+
+
   f32x4_t acc[MI][MJ];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -596,7 +644,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + D < T) issue((t + D) % NS, mbeg + (t + D) * BP);
+    if (!IL && t + D < T) issue((t + D) % NS, mbeg + (t + D) * BP);
+    const bool more = IL && t + D < T;
+    const int nslot = (t + D) % NS, nstep = mbeg + (t + D) * BP;
     // Transposed fragment reads in inline asm: hipcc treats its ds_read_tr intrinsic as
     // possibly aliasing the LDS-DMA just issued and would wait vmcnt(0) (serialising the
     // pipeline); the asm reads are ordered by hand instead: both k-slices' reads are issued,
@@ -621,6 +671,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
         fb[ks][j][1] = tr_read_asm<A_BYTES + (32 * ks + 4) * WB>(bb[j]);
       }
     });
+    constexpr int Q = KS * MI * MJ;
+    constexpr int STEP = Q / (G + 1) > 0 ? Q / (G + 1) : 1;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       if (ks + 1 < KS) lgkm_fence<(2 * (MI + MJ) > 15 ? 15 : 2 * (MI + MJ))>(fa[ks], fb[ks]);  // 4-bit counter
@@ -634,7 +686,21 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
           const bf16x8_t bfr = __builtin_bit_cast(
               bf16x8_t, __builtin_shufflevector(fb[ks][j][0], fb[ks][j][1], 0, 1, 2, 3, 4, 5, 6, 7));
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[i][j], 0, 0, 0);
+          if constexpr (IL) {
+            const int q = (ks * MI + i) * MJ + j + 1;
+            if (q % STEP == 0 && q / STEP <= G && more) {
+              __builtin_amdgcn_sched_barrier(0);
+              issue_piece(nslot, nstep, q / STEP - 1);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
         }
+    }
+    if constexpr (IL) {
+      if (Q / STEP < G && more) {
+#pragma unroll
+        for (int gp = Q / STEP; gp < G; ++gp) issue_piece(nslot, nstep, gp);
+      }
     }
     asm volatile("" ::: "memory");
   }
@@ -642,11 +708,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
   wgrad_store<MI, MJ>(a, acc, split, c0 + wc * WCO, k0 + wk * WKK, Ktot, lane);
 }
 
-template <int BKK, int BCO, int NS, int BP, bool PRO, bool BNB = false>
+template <int BKK, int BCO, int NS, int BP, bool PRO, bool BNB = false, bool IL = false>
 static int launch_wgrad_glds_p(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
   constexpr int LDS = NS * (BP * BKK * 2 + BP * BCO * 2 * (BNB ? 2 : 1)) + (BNB ? 12 * BCO : 0);
   static bool attr_set = false;
-  auto kern = conv_wgrad_glds_kernel<BKK, BCO, NS, BP, PRO, BNB>;
+  auto kern = conv_wgrad_glds_kernel<BKK, BCO, NS, BP, PRO, BNB, IL>;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
@@ -658,35 +724,38 @@ static int launch_wgrad_glds_p(DrnConvWgradArgs* a, const void* zero, hipStream_
   return (int)hipGetLastError();
 }
 
-template <int BKK, int BCO, int NS, int BP = 64>
+template <int BKK, int BCO, int NS, int BP = 64, bool IL = false>
 static int launch_wgrad_glds(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
   if (a->bnb_x != nullptr) {
-    if (a->in_scale != nullptr) return launch_wgrad_glds_p<BKK, BCO, NS, BP, true, true>(a, zero, s);
-    return launch_wgrad_glds_p<BKK, BCO, NS, BP, false, true>(a, zero, s);
+    if (a->in_scale != nullptr) return launch_wgrad_glds_p<BKK, BCO, NS, BP, true, true, IL>(a, zero, s);
+    return launch_wgrad_glds_p<BKK, BCO, NS, BP, false, true, IL>(a, zero, s);
   }
-  if (a->in_scale != nullptr) return launch_wgrad_glds_p<BKK, BCO, NS, BP, true>(a, zero, s);
-  return launch_wgrad_glds_p<BKK, BCO, NS, BP, false>(a, zero, s);
+  if (a->in_scale != nullptr) return launch_wgrad_glds_p<BKK, BCO, NS, BP, true, false, IL>(a, zero, s);
+  return launch_wgrad_glds_p<BKK, BCO, NS, BP, false, false, IL>(a, zero, s);
 }
 
-template <int NS, int BP>
+template <int NS, int BP, bool IL = false>
 static int dispatch_wgrad_tile(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
   const int Ktot = a->R * a->S * a->C;
   const bool wide_k = Ktot > 64;
   const bool wide_c = a->K > 64;
-  if (wide_k && wide_c) return launch_wgrad_glds<128, 128, NS, BP>(a, zero, s);
-  if (wide_k) return launch_wgrad_glds<128, 64, NS, BP>(a, zero, s);
-  if (wide_c) return launch_wgrad_glds<64, 128, NS, BP>(a, zero, s);
-  return launch_wgrad_glds<64, 64, NS, BP>(a, zero, s);
+  if (wide_k && wide_c) return launch_wgrad_glds<128, 128, NS, BP, IL>(a, zero, s);
+  if (wide_k) return launch_wgrad_glds<128, 64, NS, BP, IL>(a, zero, s);
+  if (wide_c) return launch_wgrad_glds<64, 128, NS, BP, IL>(a, zero, s);
+  return launch_wgrad_glds<64, 64, NS, BP, IL>(a, zero, s);
 }
 
 // pipeline id: 2 / 3 = 2 / 3 stages of 64 pixels; 4 / 5 / 6 = 2 / 3 / 4 stages of 32 pixels
-// (half the LDS per stage: more resident workgroups per CU)
+// (half the LDS per stage: more resident workgroups per CU); 7 / 8 = 2 / 3 stages of 64 pixels
+// with the interleaved LDS-DMA issue (IL)
 static int dispatch_wgrad_glds(DrnConvWgradArgs* a, const void* zero, int ns, hipStream_t s) {
   switch (ns) {
     case 3: return dispatch_wgrad_tile<3, 64>(a, zero, s);
     case 4: return dispatch_wgrad_tile<2, 32>(a, zero, s);
     case 5: return dispatch_wgrad_tile<3, 32>(a, zero, s);
     case 6: return dispatch_wgrad_tile<4, 32>(a, zero, s);
+    case 7: return dispatch_wgrad_tile<2, 64, true>(a, zero, s);
+    case 8: return dispatch_wgrad_tile<3, 64, true>(a, zero, s);
     default: return dispatch_wgrad_tile<2, 64>(a, zero, s);
   }
 }

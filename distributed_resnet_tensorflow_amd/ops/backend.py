@@ -515,7 +515,7 @@ class HipBackend(_Common):
         st = self.stream()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         best, best_t = (0, 2, False), float("inf")
-        cands = tuple(int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6").split(","))
+        cands = tuple(int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6,7,8").split(","))
         seen = set()
         modes = (False, True) if self.wgrad_atomic_ok else (False,)
         for tgt, atomic in [(t, m) for t in self.WGRAD_TARGETS for m in modes]:

@@ -310,7 +310,7 @@ WGRAD_GLDS_CASES = [
 
 
 @pytest.mark.parametrize("case", WGRAD_GLDS_CASES)
-@pytest.mark.parametrize("ns", [0, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("ns", [0, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("fused", [False, True])
 def test_conv_wgrad_pipelines(hip, ref, case, ns, fused):
     """Register-staged (ns=0) and LDS-DMA (2/3 stages) weight-gradient kernels vs fp32;
@@ -746,7 +746,7 @@ def test_conv_bnb_prologue(hip, ref, cfg, epi):
     assert rel(f.dbeta, p[0].float()) < 1e-5 and rel(f.dgamma, p[1].float()) < 1e-5
 
 
-@pytest.mark.parametrize("ns", [2, 3, 4, 5, 6])
+@pytest.mark.parametrize("ns", [2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("pro", [False, True])
 def test_wgrad_bnb_prologue(hip, ref, ns, pro):
     """1x1 weight gradient whose dY is dx of a non-materialised BN backward (BNB on the dY
@@ -767,7 +767,7 @@ def test_wgrad_bnb_prologue(hip, ref, ns, pro):
 
 
 @pytest.mark.parametrize("case", [(4, 16, 16, 16, 3, 1, 1), (4, 24, 64, 32, 1, 1, 0), (4, 33, 32, 64, 3, 2, 1)])
-@pytest.mark.parametrize("ns", [0, 2, 5])
+@pytest.mark.parametrize("ns", [0, 2, 5, 7])
 def test_wgrad_atomic_split_k(hip, ref, case, ns):
     """Split-K weight gradient accumulated with fp32 atomics straight into the (pre-zeroed)
     gradient instead of partial slabs + drn_splitk_reduce."""
