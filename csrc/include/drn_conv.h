@@ -186,11 +186,13 @@ struct DrnConvFwdArgs {
   const void* bnb_x;
   DrnBnFin bnb_fin;
   // Split-K (LDS-DMA kernels, ksplit > 1): partial-tile workspace [tiles][ksplit][BP*BC] fp32 and
-  // one zeroed ticket word per output tile (the last arriver re-arms it)
+  // one zeroed ticket word per output tile (the last arriver re-arms it).
+  // Stream-K (sk_blocks > 0): sk_blocks workgroups share the tiles x k-stages units evenly;
+  // ksplit is then the partial slots per tile (>= drn_conv_sk_slots_cfg(args, cfg, sk_blocks)).
   float* ks_ws;
   unsigned* ks_tickets;
   int32_t ksplit;
-  int32_t pad_ks_;
+  int32_t sk_blocks;
 };
 
 // dW[K][R][S][C] (+)= sum_{n,p,q} dy[n,p,q,k] * x[n, p*st-pad+r, q*st-pad+s, c]

@@ -665,7 +665,9 @@ __device__ __forceinline__ int glds_swz(int row) {
 // conv on 256 CUs) it trades 64 KB of partial traffic per extra split for a full chip.
 template <int BP, int BC, int WAVES_P, int NS, int NW = 4, bool PF = true, int BK = 64, bool PRO = false,
           bool SROW = false, bool BNB = false, int NH = 1, bool KS = false, bool IL = false>
-__global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a, const void* __restrict__ zero) {
+__device__ __forceinline__ void conv_fwd_glds_tile(const DrnConvFwdArgs& a, const void* __restrict__ zero, char* smem,
+                                                   int bid, int ksn, int ksi, int ks_stride, int t_beg_in,
+                                                   int t_cnt_in) {
   static_assert(BK == 64 || BK == 32, "k per stage");
   static_assert(!SROW || BK == 64, "row-staged narrow convs: 64-deep stages");
   static_assert(!(BNB && (PRO || SROW)), "one input transform per launch");
@@ -685,8 +687,6 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   static_assert(NS >= 2 && G * (D > 1 ? D - 1 : 1) < 64, "pipeline depth");
   static_assert(NH == 1 || (!PF && !SROW && !BNB), "sliced epilogue: big-tile plain / PRO kernels only");
 
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-
 #ifdef DRN_CONV_TRACE
   unsigned long long* const trace = g_conv_trace;
   unsigned long long t_start = 0;
@@ -700,10 +700,6 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   const int Ktot = a.R * a.S * C;
   const int ntc = (a.K + BC - 1) / BC;
   static_assert(!KS || (!SROW && !BNB), "split-K: plain / fused-BN-prologue inputs");
-  const int ksn = KS ? a.ksplit : 1;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);  // (a tile's splits stay on one XCD)
-  const int bid = KS ? lin / ksn : lin;
-  const int ksi = KS ? lin - bid * ksn : 0;
   const int tc = bid % ntc;
   const int tp = bid / ntc;
   const int m0 = tp * BP;
@@ -747,11 +743,10 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
   }
   // wave-uniform k iterator of the next stage to issue: k offset, tap (r, s), channel offset
   int ik = 0, ir = 0, is = 0, ici = 0;
-  int t_beg = 0, t_cnt = 0;  // KS: this split's k-stage range
+  int t_beg = 0, t_cnt = 0;  // KS: this split's / stream-K segment's k-stage range
   if constexpr (KS) {
-    const int t_all = Ktot / BK;
-    t_beg = (int)((long)ksi * t_all / ksn);
-    t_cnt = (int)((long)(ksi + 1) * t_all / ksn) - t_beg;
+    t_beg = t_beg_in;
+    t_cnt = t_cnt_in;
     ik = t_beg * BK;
     const int tap = ik / C;
     ici = ik - tap * C;
@@ -1040,7 +1035,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
     if (ksn > 1) {
       // publish this split's partial tile (lane-linear: 1 KB per wave-instruction), ticket
       constexpr int PER = NT * MI * MJ * 4;  // floats per partial tile (= BP * BC)
-      float* ws = a.ks_ws + (size_t)bid * ksn * PER;
+      float* ws = a.ks_ws + (size_t)bid * ks_stride * PER;
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -1101,6 +1096,70 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
 #endif
 }
 
+template <int BP, int BC, int WAVES_P, int NS, int NW = 4, bool PF = true, int BK = 64, bool PRO = false,
+          bool SROW = false, bool BNB = false, int NH = 1, bool KS = false, bool IL = false>
+__global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a, const void* __restrict__ zero) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);  // (a tile's splits stay on one XCD)
+  if constexpr (KS) {
+    const int ksn = a.ksplit;
+    const int bid = lin / ksn, ksi = lin - bid * ksn;
+    const int t_all = (a.R * a.S * a.C) / BK;
+    const int t_beg = (int)((long)ksi * t_all / ksn);
+    const int t_cnt = (int)((long)(ksi + 1) * t_all / ksn) - t_beg;
+    conv_fwd_glds_tile<BP, BC, WAVES_P, NS, NW, PF, BK, PRO, SROW, BNB, NH, KS, IL>(a, zero, smem, bid, ksn, ksi, ksn,
+                                                                                  t_beg, t_cnt);
+  } else {
+    conv_fwd_glds_tile<BP, BC, WAVES_P, NS, NW, PF, BK, PRO, SROW, BNB, NH, KS, IL>(a, zero, smem, lin, 1, 0, 1, 0, 0);
+  }
+}
+
+// Stream-K (a.sk_blocks = gridDim.x > 0): the U = tiles x k-stages units are cut into gridDim.x
+// equal contiguous ranges, one per workgroup; a workgroup walks the tile segments of its range
+// (tile-major, k-minor). A tile whose units span several workgroups is finished by its last
+// arriving contributor (partials summed in contributor order: bitwise reproducible); nobody
+// waits. Every CU gets the same number of MFMA k-stages whatever the tile count (98 / 196 / 392
+// tiles of the ResNet-50 layers against 256 CUs).
+template <int BP, int BC, int WAVES_P, int NS, int NW = 4, int BK = 64, bool PRO = false, int NH = 1, bool IL = false>
+__global__ __launch_bounds__(NW * 64) void conv_fwd_glds_sk_kernel(DrnConvFwdArgs a, const void* __restrict__ zero) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  // (32-bit unit arithmetic: the launcher checks tiles x k-stages x grid < 2^31)
+  const unsigned G = gridDim.x;
+  const unsigned b = xcd_remap(blockIdx.x, G);  // consecutive ranges (shared tiles) on one XCD
+  const unsigned M = a.N * a.P * a.Q;
+  const unsigned tiles = ((M + BP - 1) / BP) * ((a.K + BC - 1) / BC);
+  const unsigned t_all = (a.R * a.S * a.C) / BK;
+  const unsigned U = tiles * t_all;
+  auto owner = [&](unsigned u) { return ((u + 1) * G - 1) / U; };  // workgroup whose range holds unit u
+  unsigned u = __builtin_amdgcn_readfirstlane(b * U / G);
+  const unsigned uend = __builtin_amdgcn_readfirstlane((b + 1) * U / G);
+  bool first = true;
+  while (u < uend) {
+    const unsigned tile = __builtin_amdgcn_readfirstlane(u / t_all);
+    const unsigned tbase = tile * t_all;
+    const unsigned tend = tbase + t_all;
+    const unsigned t0 = u - tbase, t1 = (tend < uend ? tend : uend) - tbase;  // (uniform)
+    const unsigned bf = __builtin_amdgcn_readfirstlane(owner(tbase));
+    const unsigned bl = __builtin_amdgcn_readfirstlane(owner(tend - 1));
+    if (!first) __syncthreads();  // the previous segment's LDS use is over
+    // (no epilogue-operand prefetch: most segments end in a partial tile, not an epilogue)
+    conv_fwd_glds_tile<BP, BC, WAVES_P, NS, NW, false, BK, PRO, false, false, NH, true, IL>(
+        a, zero, smem, (int)tile, (int)(bl - bf + 1), (int)(b - bf), a.ksplit, (int)t0, (int)(t1 - t0));
+    first = false;
+    u = tend;
+  }
+}
+
+// partial-tile slots a stream-K launch needs per tile: the most ranges (of >= floor(U / G) units)
+// one tile's T units can touch; 0 = invalid (more workgroups than units: empty ranges)
+static int sk_slots(int tiles, int T, int G) {
+  const long U = (long)tiles * T;
+  if (G < 1 || T < 1 || U < G || U * (long)(G + 1) >= (1l << 31)) return 0;
+  const long L = U / G;
+  const long n = (T - 1 + L - 1) / L + 1;
+  return (int)(n < G ? n : G);
+}
+
 // largest grid that finalizes its input BatchNorm in the prologue (DRN_CFIN_MAX_BLOCKS)
 static int cfin_max_blocks() {
   static int v = -1;
@@ -1130,6 +1189,22 @@ static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t 
   const int tiles_p = (M + BP - 1) / BP;
   const int tiles_c = (a->K + BC - 1) / BC;
   a->tiles_p = tiles_p;
+  if constexpr (KS) {
+    if (a->sk_blocks > 0) {  // stream-K: sk_blocks workgroups, ksplit = partial slots per tile
+      if (a->ks_ws == nullptr || a->ks_tickets == nullptr) return (int)hipErrorInvalidValue;
+      const int need = sk_slots(tiles_p * tiles_c, T, a->sk_blocks);
+      if (need == 0 || need > a->ksplit) return (int)hipErrorInvalidValue;
+      auto skern = conv_fwd_glds_sk_kernel<BP, BC, WAVES_P, NS, NW, BK, PRO, NH, IL>;
+      static bool sk_attr_set = false;
+      if (!sk_attr_set) {
+        hipFuncSetAttribute(reinterpret_cast<const void*>(skern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+        sk_attr_set = true;
+      }
+      hipLaunchKernelGGL(skern, dim3(a->sk_blocks), dim3(NW * 64), LDS, stream, *a, zero);
+      return (int)hipGetLastError();
+    }
+  }
   const int ks = KS ? a->ksplit : 1;
   if (KS && (ks < 2 || T < ks || a->ks_ws == nullptr || a->ks_tickets == nullptr)) return (int)hipErrorInvalidValue;
   if (PRO && a->in_fin.stats != nullptr && tiles_p * tiles_c * ks > cfin_max_blocks()) {
@@ -1168,7 +1243,7 @@ static int launch_conv_glds_ks(DrnConvFwdArgs* a, const void* zero, hipStream_t 
 // epilogue operands (residual / BN-backward input) are prefetched only when present
 template <int BP, int BC, int WAVES_P, int NS, int NW = 4, int BK = 64, int NH = 1, bool IL = false, bool KSOK = false>
 static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
-  if (a->ksplit > 1) {
+  if (a->ksplit > 1 || a->sk_blocks > 0) {
     if constexpr (KSOK) return launch_conv_glds_ks<BP, BC, WAVES_P, NS, NW, BK, NH, IL>(a, zero, stream);
     return (int)hipErrorInvalidValue;
   }
@@ -1281,6 +1356,18 @@ static int glds_cfg_bp(int cfg) {
   }
 }
 
+static int glds_cfg_bk(int cfg) {
+  switch (cfg) {
+#define DRN_X(id, bp, bc, wpv, ns, nw, bk, nh, il, ks) \
+  case id:                                             \
+    return ks ? bk : 0;
+    DRN_GLDS_CONFIGS(DRN_X)
+#undef DRN_X
+    default:
+      return 0;
+  }
+}
+
 static int glds_cfg_bc(int cfg) {
   switch (cfg) {
 #define DRN_X(id, bp, bc, wpv, ns, nw, bk, nh, il, ks) \
@@ -1372,7 +1459,8 @@ DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
   if (a->in_fin.stats != nullptr &&
       (a->in_scale == nullptr || a->in_fin.C != a->C || a->in_fin.G < 1 || a->in_fin.G > DRN_BN_FIN_GMAX))
     return (int)hipErrorInvalidValue;
-  if (a->ksplit > 1 && (a->cfg < 0 || a->cfg >= DRN_GLDS_NCFG || !drn_conv_glds_ok(a) || zero == nullptr))
+  if ((a->ksplit > 1 || a->sk_blocks > 0) &&
+      (a->cfg < 0 || a->cfg >= DRN_GLDS_NCFG || !drn_conv_glds_ok(a) || zero == nullptr))
     return (int)hipErrorInvalidValue;  // split-K: explicit split-capable LDS-DMA configurations only
   if (a->cfg >= DRN_GLDS_NCFG && a->cfg != 100) return drn_conv_mt(a->cfg - DRN_GLDS_NCFG, a, zero, s);
   if (a->bnb_x != nullptr && (!drn_conv_glds_ok(a) || zero == nullptr || a->cfg == 100))
@@ -1400,6 +1488,15 @@ DRN_API int drn_conv_trace_set(unsigned long long* buf) {
 
 DRN_API int drn_conv_glds_cfg_bp(int cfg) { return drn::glds_cfg_bp(cfg); }
 DRN_API int drn_conv_glds_cfg_bc(int cfg) { return drn::glds_cfg_bc(cfg); }
+// partial slots per tile a stream-K launch of split-capable config cfg with G workgroups needs
+// (0: not split-capable, or more workgroups than tile x k-stage units)
+DRN_API int drn_conv_sk_slots_cfg(const DrnConvFwdArgs* a, int cfg, int G) {
+  const int bk = drn::glds_cfg_bk(cfg);
+  if (bk == 0 || (a->R * a->S * a->C) % bk) return 0;
+  const int M = a->N * a->P * a->Q;
+  const int bp = drn::glds_cfg_bp(cfg), bc = drn::glds_cfg_bc(cfg);
+  return drn::sk_slots(((M + bp - 1) / bp) * ((a->K + bc - 1) / bc), (a->R * a->S * a->C) / bk, G);
+}
 DRN_API int drn_conv_glds_num_cfgs() { return DRN_GLDS_NCFG + drn_conv_mt_num_cfgs(); }
 DRN_API int drn_conv_glds_default_cfg(const DrnConvFwdArgs* a) { return drn::glds_default_cfg(a); }
 

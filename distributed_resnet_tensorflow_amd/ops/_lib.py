@@ -64,7 +64,7 @@ class DrnConvFwdArgs(ctypes.Structure):
         ("fin_dgamma", c_p), ("fin_dbeta", c_p), ("fin_coef", c_p),
         ("fd_pq", DrnFastDiv), ("fd_q", DrnFastDiv), ("in_fin", DrnBnFin),
         ("bnb_x", c_p), ("bnb_fin", DrnBnFin),
-        ("ks_ws", c_p), ("ks_tickets", c_p), ("ksplit", c_int), ("pad_ks_", c_int),
+        ("ks_ws", c_p), ("ks_tickets", c_p), ("ksplit", c_int), ("sk_blocks", c_int),
     ]
 
 
@@ -125,6 +125,7 @@ _SIGS = {
     "drn_p2p_cast": ([c_p, c_p, c_i64, c_p], c_int),
     "drn_p2p_args_size": ([], c_int),
     "drn_conv_glds_cfg_bc": ([c_int], c_int),
+    "drn_conv_sk_slots_cfg": ([c_p, c_int, c_int], c_int),
     "drn_p2p_alloc": ([ctypes.POINTER(c_p), ctypes.c_size_t], c_int),
     "drn_p2p_free": ([c_p], c_int),
     "drn_bn_fin_size": ([], c_int),

@@ -232,6 +232,8 @@ class HipBackend(_Common):
         self.ks_ws = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.ks_tickets = torch.zeros(1 << 16, dtype=torch.int32, device=self.device)
         self.KS_FACTORS = tuple(int(v) for v in os.environ.get("DRN_CONV_KSPLIT", "2,3,4").split(",") if v)
+        # stream-K grid sizes tried by the autotuner (256 CUs: 1 or 2 resident workgroups each)
+        self.SK_BLOCKS = tuple(int(v) for v in os.environ.get("DRN_CONV_SK", "256,512").split(",") if v)
         forced = os.environ.get("DRN_CONV_CFG")
         self.forced_cfg = int(forced) if forced not in (None, "") else None
         self.autotune = os.environ.get("DRN_AUTOTUNE", "1") == "1"
@@ -318,9 +320,18 @@ class HipBackend(_Common):
         return ((M + bp - 1) // bp) * ((a.K + bc - 1) // bc) * ks * bp * bc
 
     def _set_ksplit(self, a, ks: int):
+        """ks > 1: split-K factor; ks < 0: stream-K over -ks workgroups (DrnConvFwdArgs.sk_blocks;
+        ksplit then holds the partial slots per tile the launch needs)."""
+        a.sk_blocks = 0
         a.ksplit = int(ks) if ks and ks > 1 else 0
-        if a.ksplit > 1:
-            need = self._ks_need(a, a.ksplit)
+        if ks and ks < 0:
+            a.sk_blocks = -int(ks)
+            a.ksplit = self.L.drn_conv_sk_slots_cfg(ctypes.byref(a), a.cfg, a.sk_blocks)
+            if a.ksplit == 0:  # not applicable: leave it to the library to refuse the launch
+                a.ks_ws = a.ks_tickets = None
+                return
+        if a.ksplit > 1 or a.sk_blocks:
+            need = self._ks_need(a, max(1, a.ksplit))
             if need > self.ks_ws.numel():
                 if torch.cuda.is_current_stream_capturing():
                     raise RuntimeError("split-K workspace must be sized before graph capture (autotune first)")
@@ -395,6 +406,8 @@ class HipBackend(_Common):
                 tiles = ((M + bp - 1) // bp) * ((a.K + bc - 1) // bc)
                 if tiles < 512:
                     pairs += [(cfg, k) for k in self.KS_FACTORS if k > 1]
+                if tiles < 1024:  # stream-K: every CU gets the same share of tile k-stages
+                    pairs += [(cfg, -g) for g in self.SK_BLOCKS if self.L.drn_conv_sk_slots_cfg(ctypes.byref(a), cfg, g)]
         # pass 1: every applicable configuration, short; pass 2: the 4 fastest re-timed twice,
         # interleaved, keeping each one's best (single short timings picked outliers: clock
         # ramps and neighbours' cache state moved the choice by >10 %)
@@ -440,7 +453,9 @@ class HipBackend(_Common):
         bco = 128 if K > 64 else 64
         tiles = ((Ktot + bkk - 1) // bkk) * ((K + bco - 1) // bco)
         steps = (M + 63) // 64
-        want = max(1, min((target_blocks + tiles - 1) // tiles, max(1, steps // min_steps)))
+        # never MORE blocks than the target (rounding the split count up made e.g. 36 tiles x 15
+        # splits = 540 blocks for a 512-slot target: 28 blocks ran as a second wave, alone)
+        want = max(1, min(target_blocks // tiles, max(1, steps // min_steps)))
         per = (steps + want - 1) // want
         splits = (steps + per - 1) // per
         return splits, per * 64
@@ -448,7 +463,7 @@ class HipBackend(_Common):
     # split-K block targets the wgrad autotuner chooses from per geometry: more splits fill the
     # chip, fewer write (and re-read in drn_splitk_reduce) fewer fp32 partial slabs -- the slab
     # traffic of the default 512-block target is ~1.7 GB per ResNet-50 step
-    WGRAD_TARGETS = tuple(int(v) for v in os.environ.get("DRN_WGRAD_TARGETS", "128,256,512").split(","))
+    WGRAD_TARGETS = tuple(int(v) for v in os.environ.get("DRN_WGRAD_TARGETS", "128,256,384,512,768").split(","))
 
     def wgrad_args(self, x, dy, out, g: ConvGeom, in_bn=None, relu_in=True, ws=None, target_blocks: int = 0,
                    bnb=None, atomic: bool = False):

@@ -41,13 +41,14 @@ if "stats" in flags:
     kw["stats"] = torch.zeros(8, 2, K, device="cuda")
 out = []
 for cfg in [100] + list(range(be.L.drn_conv_glds_num_cfgs())):
-    for ks in (1, 2, 3, 4):  # split-K factors (only the split-capable configurations accept ks > 1)
+    # split-K factors / stream-K grids (< 0; only the split-capable configurations accept them)
+    for ks in (1, 2, 3, 4, -256, -512):
         a = be.conv_args(x, w, y, g, **kw)
         a.cfg = cfg
         be._set_ksplit(a, ks)
         if be.L.drn_conv_fwd2(ctypes.byref(a), be.zero_page.data_ptr(), be.stream()) != 0:
             continue
         t = timeit(lambda: be.L.drn_conv_fwd2(ctypes.byref(a), be.zero_page.data_ptr(), be.stream()))
-        out.append((t, f"{cfg}" if ks == 1 else f"{cfg}/k{ks}"))
+        out.append((t, f"{cfg}" if ks == 1 else f"{cfg}/k{ks}" if ks > 1 else f"{cfg}/sk{-ks}"))
 out.sort()
 print(f"N{N} H{H} C{C} K{K} R{R} s{st} {sorted(flags)}: " + " ".join(f"{c}:{t:.1f}" for t, c in out[:14]), flush=True)

@@ -7,15 +7,20 @@ OUT=${1:-gpurun_out/diag}
 export PYTHONPATH=$(pwd)
 mkdir -p "$OUT"
 set -o pipefail
-echo "== kernel_bench"
-timeout -k 10 300 python -u scripts/kernel_bench.py --iters 10 --pro --no_bn --json "$OUT/kernel_bench.json" \
-  > "$OUT/kernel_bench.txt" 2>&1 || { tail "$OUT/kernel_bench.txt"; exit 1; }
-tail -25 "$OUT/kernel_bench.txt"
+if [ -n "$KBENCH" ]; then
+  echo "== kernel_bench"
+  timeout -k 10 300 python -u scripts/kernel_bench.py --iters 10 --pro --no_bn --json "$OUT/kernel_bench.json" \
+    > "$OUT/kernel_bench.txt" 2>&1 || { tail "$OUT/kernel_bench.txt"; exit 1; }
+  tail -25 "$OUT/kernel_bench.txt"
+fi
+if [ -n "$ENVAB" ]; then
+  echo "== env A/B (eager steps)"
+  SWEEP_ARGS="--graph 0" timeout -k 10 600 bash scripts/env_sweep.sh "$OUT/env_ab.txt" $ENVAB || exit 1
+fi
 echo "== conv timelines"
 if [ -f gpu_variants/trace/libdrn_kernels.so ]; then
-  for spec in "14 256 256 3 1 0 stats" "14 256 256 3 1 8 stats" "14 256 256 3 1 25 stats" "14 256 256 3 1 27 stats" \
-              "7 512 2048 1 1 26 pro res stats" "7 512 2048 1 1 10 pro res stats" "7 512 512 3 1 13 pro stats" \
-              "28 128 512 1 1 21 pro res stats" "28 128 512 1 1 25 pro res stats"; do
+  for spec in ${TRACES:-"14 256 256 3 1 0 stats" "14 256 256 3 1 31 stats" "14 256 256 3 1 25 stats" "14 256 256 3 1 33 stats" \
+              "14 256 256 3 1 8 stats" "14 256 256 3 1 34 stats"}; do
     DRN_KERNEL_LIB=gpu_variants/trace/libdrn_kernels.so timeout -k 10 60 python -u scripts/trace_conv.py $spec \
       2>&1 | grep --line-buffered -v amdgpu.ids | tee -a "$OUT/timelines.txt" || exit 1
   done
@@ -23,6 +28,9 @@ fi
 if [ -n "$PROBES" ]; then
   echo "== cifar eval probe"
   timeout -k 10 500 bash scripts/probes/cifar_eval_probe.sh "$OUT/cifar" 2>&1 | grep --line-buffered -v amdgpu.ids | tee "$OUT/cifar_probe.txt" || exit 1
+  echo "== ImageNet host input rate (this box's CPUs)"
+  timeout -k 10 300 python -u scripts/imagenet_input_bench.py --images 2048 --threads 4,8,16 --workers thread,process \
+    2>&1 | grep --line-buffered -v amdgpu.ids | tee "$OUT/imagenet_input.txt" || exit 1
   echo "== queue audit"
   timeout -k 10 400 bash scripts/queue_audit.sh "$OUT/queue" 2>&1 | grep --line-buffered -v amdgpu.ids | tee "$OUT/queue_audit.txt" || exit 1
   echo "== p2p failure tests"

@@ -1,10 +1,11 @@
 """End-to-end runs of the reference-named entry points on the GPU (HIP kernels, HIP-graph step):
 
   * resnet_cifar_main.py --num_gpus=1 on a class-conditional fake CIFAR-10 (learnable: one hue
-    per class) -> checkpoint -> resnet_cifar_eval.py --eval_once=True --num_gpus=1 must report
-    training precision >= 0.95 and held-out precision > 0.75 (chance: 0.1) -- convergence of
-    the whole GPU train + eval path;
-    accuracy parity with the reference's 93 % on real CIFAR-10 is unpinned: no dataset here);
+    per class) with the reference LR schedule compressed 20x (--lr_schedule_scale=0.05: 0.1,
+    0.01 from step 2000, 0.001 from 3000) -> checkpoint -> resnet_cifar_eval.py --eval_once=True
+    must report held-out precision >= 0.95 and >= 0.98 on the training records -- convergence
+    of the whole GPU train + eval path (accuracy parity with the reference's 93 % on real
+    CIFAR-10 is unpinned: no dataset here);
   * resnet_imagenet_main.py / resnet_imagenet_eval.py on fake TFRecord shards (default model =
     ResNet-v2-50) -> checkpoint -> eval.
 """
@@ -39,23 +40,27 @@ def test_cifar_gpu_train_checkpoint_eval_converges(tmp_path):
     write_fake_cifar(data, 1000, learnable=True)
     ck, ev = str(tmp_path / "ck"), str(tmp_path / "ev")
     out = run(["resnet_cifar_main.py", "--num_gpus=1", f"--train_data_path={data}", f"--log_root={ck}",
-               "--resnet_size=8", "--batch_size=128", "--train_steps=2000", "--log_every_n_steps=50"])
-    assert "global step 2000" in out, out[-2000:]
-    assert os.path.exists(os.path.join(ck, "model.ckpt-2000.index"))
+               "--resnet_size=8", "--batch_size=128", "--train_steps=3000", "--lr_schedule_scale=0.05",
+               "--log_every_n_steps=50"])
+    assert "global step 3000" in out, out[-2000:]
+    assert os.path.exists(os.path.join(ck, "model.ckpt-3000.index"))
     train_prec = [float(v) for v in re.findall(r"precision = ([0-9.]+)", out)]
     assert train_prec and max(train_prec[-5:]) >= 0.95, out[-2000:]
-    out = run(["resnet_cifar_eval.py", "--mode=eval", "--eval_once=True", "--num_gpus=1",
-               f"--eval_data_path={data}/cifar-10-batches-bin/test_batch*", f"--log_root={ck}", f"--eval_dir={ev}",
-               "--resnet_size=8", "--eval_batch_count=10"])
-    m = re.findall(r"precision: ([0-9.]+), best precision", out)
-    assert m, out[-2000:]
-    # eval uses the BN MOVING statistics (decay 0.997, reference resnet_model_official.py:37),
-    # which lag the weights trained at a constant 0.1 learning rate: over repeated runs whose
-    # training precision is 1.0 the held-out precision measured 0.79-1.0 (re-evaluating one
-    # checkpoint is deterministic), so the bar is "far above chance (0.1)", not a fixed 0.9
-    assert float(m[-1]) > 0.75, out[-2000:]
-    best = json.load(open(os.path.join(ev, "best_precision.json")))
-    assert best["step"] == 2000 and best["best_precision"] > 0.75
+    # Eval normalises with the BN MOVING statistics (decay 0.997, reference
+    # resnet_model_official.py:37). Root cause of the round-2 spread (0.67-1.0 held out, the SAME
+    # on the training records, batch-statistics precision 1.0: scripts/probes/cifar_eval_probe.sh,
+    # profiles/r3_cifar_eval_probe.txt): at a constant LR of 0.1 the weights keep moving faster
+    # than a 0.997 average (~330-step horizon) can follow; the reference only evaluates after its
+    # 40k/60k-step decays. With the compressed schedule the averages catch up.
+    for name, pattern, bar in (("test", "test_batch*", 0.95), ("train", "data_batch_*", 0.98)):
+        out = run(["resnet_cifar_eval.py", "--mode=eval", "--eval_once=True", "--num_gpus=1",
+                   f"--eval_data_path={data}/cifar-10-batches-bin/{pattern}", f"--log_root={ck}",
+                   f"--eval_dir={ev}_{name}", "--resnet_size=8", "--eval_batch_count=10"])
+        m = re.findall(r"precision: ([0-9.]+), best precision", out)
+        assert m, out[-2000:]
+        assert float(m[-1]) >= bar, (name, out[-2000:])
+    best = json.load(open(os.path.join(ev + "_test", "best_precision.json")))
+    assert best["step"] == 3000 and best["best_precision"] >= 0.95
 
 
 @pytest.mark.timeout(600)

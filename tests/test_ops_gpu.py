@@ -180,6 +180,64 @@ def test_conv_fwd_splitk(hip, ref, case, cfg, ks):
     assert int(hip.ks_tickets.abs().sum()) == 0  # every ticket re-armed by its last arriver
 
 
+@pytest.mark.parametrize("case", SPLITK_CASES)
+@pytest.mark.parametrize("cfg", KS)
+@pytest.mark.parametrize("G", [3, 7, 16])
+def test_conv_fwd_streamk(hip, ref, case, cfg, G):
+    """Stream-K launches (G workgroups share the tiles x k-stages units evenly; a tile spread
+    over several workgroups is finished by its last arriver) vs the fp32 reference, bitwise
+    equal across two launches, every ticket re-armed."""
+    N, H, W, C, K, R, s, p = case
+    torch.manual_seed(40 + G)
+    P = out_size(H, R, s, p)
+    x = bf(torch.randn(N, H, W, C))
+    w = bf(torch.randn(K, R, R, C) * (2.0 / (R * R * C)) ** 0.5)
+    res = bf(torch.randn(N, P, P, K))
+    g = ConvGeom(stride=s, pad_h=p, pad_w=p)
+    in_bn = (torch.rand(C) + 0.5, torch.randn(C) * 0.5)
+    y_ref = torch.zeros(N, P, P, K)
+    st_ref = torch.zeros(2 * K)
+    ref.conv_fwd(x.float(), w.float(), y_ref, g, in_bn=in_bn, residual=res.float(), stats=st_ref)
+    outs = []
+    for _ in range(2):
+        y = torch.zeros(N, P, P, K, dtype=torch.bfloat16, device="cuda")
+        st = torch.zeros(3, 2, K, device="cuda")
+        a = hip.conv_args(x.cuda(), w.cuda(), y, g, residual=res.cuda(), stats=st,
+                          in_bn=(in_bn[0].cuda(), in_bn[1].cuda()))
+        a.cfg = cfg
+        slots = hip.L.drn_conv_sk_slots_cfg(ctypes.byref(a), cfg, G)
+        hip._set_ksplit(a, -G)
+        rc = hip.L.drn_conv_fwd2(ctypes.byref(a), hip.zero_page.data_ptr(), hip.stream())
+        if slots == 0:
+            assert rc != 0, (cfg, G)  # more workgroups than units: refused
+            return
+        assert rc == 0 and 1 <= slots <= G
+        torch.cuda.synchronize()
+        assert rel(y, y_ref) < 1e-2, (cfg, G)
+        s_hip = st.sum(0).view(-1).cpu()
+        assert rel(s_hip[:K], st_ref[:K]) < 2e-2
+        assert rel(s_hip[K:], st_ref[K:]) < 2e-2
+        outs.append(y.clone())
+    assert torch.equal(outs[0], outs[1])
+    assert int(hip.ks_tickets.abs().sum()) == 0
+
+
+def test_conv_sk_slots(hip):
+    """The stream-K slot count bounds how many workgroups one tile's k-stages can touch."""
+    a = hip.conv_args(torch.zeros(2, 9, 9, 64, dtype=torch.bfloat16, device="cuda"),
+                      torch.zeros(128, 3, 3, 64, dtype=torch.bfloat16, device="cuda"),
+                      torch.zeros(2, 9, 9, 128, dtype=torch.bfloat16, device="cuda"), ConvGeom(1, 1, 1))
+    # config 0: 128x128 tiles, 64-deep stages -> 2 tiles x 9 stages = 18 units
+    for G in range(1, 19):
+        starts = [b * 18 // G for b in range(G)] + [18]
+        touch = max(sum(1 for b in range(G) if starts[b] < (t + 1) * 9 and starts[b + 1] > t * 9) for t in range(2))
+        slots = hip.L.drn_conv_sk_slots_cfg(ctypes.byref(a), 0, G)
+        assert touch <= slots <= touch + 1, (G, touch, slots)  # a safe, near-tight bound
+    assert hip.L.drn_conv_sk_slots_cfg(ctypes.byref(a), 0, 18) == 9   # one unit per workgroup
+    assert hip.L.drn_conv_sk_slots_cfg(ctypes.byref(a), 0, 19) == 0   # empty ranges refused
+    assert hip.L.drn_conv_sk_slots_cfg(ctypes.byref(a), 1, 4) == 0    # not split-capable
+
+
 def test_conv_glds_out_map(hip, ref):
     """Phase output mapping (stride-2 data-gradient phases) through the LDS-DMA kernel."""
     torch.manual_seed(5)
