@@ -1150,14 +1150,246 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_sk_kernel(DrnConvFwdArg
   }
 }
 
-// partial-tile slots a stream-K launch needs per tile: the most ranges (of >= floor(U / G) units)
-// one tile's T units can touch; 0 = invalid (more workgroups than units: empty ranges)
+// ---------------- narrow-output convs (K = 16 / 32): operands straight to registers ----------------
+// The CIFAR stage-1 convs (64 -> 16 1x1, 16 -> 16 3x3 and their data gradients; reference
+// resnet_model_official.py:255-266, 16 filters per stage-1 bottleneck) have so few output channels
+// that an LDS-staged tile is mostly overhead: the weights are 2-9 KB and each pixel row feeds one
+// 16-channel MFMA column. Here a wave owns WP = 16 MJ output pixels x 16 MI channels; the A
+// fragments (weights, every k-step) are loaded into registers once, the B fragments (8 channels
+// of one pixel per lane: one 16-byte load, zero for padding) come straight from global memory,
+// every k-step issued before the first MFMA (the kernel is bandwidth-bound: bytes in flight
+// decide). A k-step is 32 k; with C < 32 it spans 32 / C taps (taps paired, not channels padded).
+// The fused BN-apply (+ReLU) prologue runs on the fragments in registers (its per-channel
+// parameters staged in LDS behind the epilogue tile); the epilogue is the shared LDS-staged one
+// (residual, statistics, BN-backward reduction, finalize).
+template <int MI, int MJ, int NW, int KMAX, bool PRO>
+__global__ __launch_bounds__(NW * 64) void conv_fwd_nk_kernel(DrnConvFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NT = NW * 64, WP = 16 * MJ, BP = WP * NW, BC = 16 * MI;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4;
+  const int M = a.N * a.P * a.Q;
+  const int C = a.C, RS = a.R * a.S;
+  const int Ktot = RS * C;
+  const int ksteps = (Ktot + 31) >> 5;
+  const int cshift = __builtin_ctz(C);  // (the launcher requires a power-of-two C)
+  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * BP;
+  const bf16_t* __restrict__ xg = reinterpret_cast<const bf16_t*>(a.x);
+  const bf16_t* __restrict__ wg = reinterpret_cast<const bf16_t*>(a.w);
+  float* ssl = reinterpret_cast<float*>(smem + BP * BC * 4);  // [scale C][shift C]
+  if constexpr (PRO) {
+    if (a.in_fin.stats != nullptr) {
+      // consumer-side BN finalize straight from the statistics replicas (the first workgroup of
+      // a publishing launch also writes scale / shift out for later kernels)
+      const bool pub = a.in_fin.publish && blockIdx.x == 0;
+      for (int c = tid; c < C; c += NT) drn_bn_fin_fwd(a.in_fin, c, pub, ssl[c], ssl[C + c]);
+    } else {
+      for (int c = tid; c < C; c += NT) {
+        ssl[c] = a.in_scale[c];
+        ssl[C + c] = a.in_shift[c];
+      }
+    }
+  }
+  // this lane's output pixels
+  int pb[MJ], ph[MJ], pw[MJ];
+#pragma unroll
+  for (int j = 0; j < MJ; ++j) {
+    const int m = m0 + wave * WP + j * 16 + (lane & 15);
+    if (m < M) {
+      const int n = (int)drn_fdiv((uint32_t)m, a.fd_pq);
+      const int rem = m - n * (a.P * a.Q);
+      const int p = (int)drn_fdiv((uint32_t)rem, a.fd_q);
+      const int q = rem - p * a.Q;
+      ph[j] = p * a.stride - a.pad_h;
+      pw[j] = q * a.stride - a.pad_w;
+      pb[j] = ((n * a.H + ph[j]) * a.W + pw[j]) * C;
+    } else {
+      ph[j] = -(1 << 28);
+      pw[j] = 0;
+      pb[j] = 0;
+    }
+  }
+  // every k-step's B fragments in flight first, then the weights
+  uint4 xb[KMAX][MJ];
+  unsigned long long okm = 0;  // bit t * MJ + j: fragment (t, j) inside the input (PRO: transform it)
+#pragma unroll
+  for (int t = 0; t < KMAX; ++t) {
+    if (t < ksteps) {
+      const int k = t * 32 + g * 8;
+      const int tap = k >> cshift;
+      const int ci = k - (tap << cshift);
+      const int r = tap / a.S, sx = tap - r * a.S;
+#pragma unroll
+      for (int j = 0; j < MJ; ++j) {
+        const int h = ph[j] + r, w = pw[j] + sx;
+        const bool ok = tap < RS && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+        xb[t][j] = ok ? *reinterpret_cast<const uint4*>(xg + pb[j] + (r * a.W + sx) * C + ci)
+                      : make_uint4(0u, 0u, 0u, 0u);
+        if (ok) okm |= 1ull << (t * MJ + j);
+      }
+    }
+  }
+  bf16x8_t wa[MI][KMAX];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int t = 0; t < KMAX; ++t) {
+      const int k = t * 32 + g * 8;
+      const uint4 v = (t < ksteps && k < Ktot)
+                          ? *reinterpret_cast<const uint4*>(wg + (size_t)(i * 16 + (lane & 15)) * Ktot + k)
+                          : make_uint4(0u, 0u, 0u, 0u);
+      wa[i][t] = __builtin_bit_cast(bf16x8_t, v);
+    }
+  if constexpr (PRO) __syncthreads();  // BN parameters staged
+  f32x4_t acc[MI][MJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < KMAX; ++t) {
+    if (t < ksteps) {
+      bf16x8_t bv[MJ];
+      if constexpr (PRO) {
+        const int k = t * 32 + g * 8;
+        const int ci = k & (C - 1);
+        float sc[8], sh[8];
+#pragma unroll
+        for (int e = 0; e < 8; e += 4) {
+          const float4 s4 = *reinterpret_cast<const float4*>(ssl + ci + e);
+          const float4 h4 = *reinterpret_cast<const float4*>(ssl + C + ci + e);
+          sc[e] = s4.x, sc[e + 1] = s4.y, sc[e + 2] = s4.z, sc[e + 3] = s4.w;
+          sh[e] = h4.x, sh[e + 1] = h4.y, sh[e + 2] = h4.z, sh[e + 3] = h4.w;
+        }
+#pragma unroll
+        for (int j = 0; j < MJ; ++j) {
+          float f[8];
+          unpack8(xb[t][j], f);
+          const bool ok = (okm >> (t * MJ + j)) & 1ull;  // padding stays zero (BN-apply first)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float v = f[e] * sc[e] + sh[e];
+            if (a.relu_in) v = v > 0.f ? v : 0.f;
+            f[e] = ok ? v : 0.f;
+          }
+          bv[j] = __builtin_bit_cast(bf16x8_t, pack8(f));
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < MJ; ++j) bv[j] = __builtin_bit_cast(bf16x8_t, xb[t][j]);
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < MJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i][t], bv[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  EpiPre<BP, BC, NT, false> e;
+  epi_prefetch<BP, BC, NT, false>(a, m0, 0, M, e);
+  conv_epilogue<BP, BC, WP, BC, MI, MJ, NT, false>(a, smem, acc, wave, 0, m0, 0, M, e);
+}
+
+static int cfin_max_blocks();
+
+// id -> (MI, MJ): 16-channel outputs with 32 / 64 pixels per wave, 32-channel with 16 / 32 / 64
+#define DRN_NK_CONFIGS(X) X(0, 1, 2) X(1, 1, 4) X(2, 2, 1) X(3, 2, 2) X(4, 2, 4)
+#define DRN_NK_NCFG 5
+#define DRN_NK_CFG0 200  // configuration id of NK config 0 (DrnConvFwdArgs::cfg)
+
+template <int MI, int MJ, bool PRO, int KMAX>
+static int launch_conv_nk_k(DrnConvFwdArgs* a, hipStream_t stream) {
+  constexpr int NW = 4, BP = 16 * MJ * NW, BC = 16 * MI;
+  static_assert(BP % (NW * 64 / (BC / 8)) == 0, "epilogue rows per pass must divide the tile");
+  const int M = a->N * a->P * a->Q;
+  const int LDS = BP * BC * 4 + (PRO ? 8 * a->C : 0);
+  if (LDS > 160 * 1024) return (int)hipErrorInvalidValue;
+  auto kern = conv_fwd_nk_kernel<MI, MJ, NW, KMAX, PRO>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  a->tiles_p = (M + BP - 1) / BP;
+  hipLaunchKernelGGL(kern, dim3(a->tiles_p), dim3(NW * 64), LDS, stream, *a);
+  return (int)hipGetLastError();
+}
+
+template <int MI, int MJ, bool PRO>
+static int launch_conv_nk_p(DrnConvFwdArgs* a, hipStream_t stream) {
+  const int ksteps = (a->R * a->S * a->C + 31) / 32;
+  if (ksteps <= 2) return launch_conv_nk_k<MI, MJ, PRO, 2>(a, stream);
+  if (ksteps <= 5) return launch_conv_nk_k<MI, MJ, PRO, 5>(a, stream);
+  if (ksteps <= 9) return launch_conv_nk_k<MI, MJ, PRO, 9>(a, stream);
+  return (int)hipErrorInvalidValue;
+}
+
+static int nk_cfg_mi(int id) {
+  switch (id) {
+#define DRN_X(id, mi, mj) \
+  case id:                \
+    return mi;
+    DRN_NK_CONFIGS(DRN_X)
+#undef DRN_X
+    default:
+      return 0;
+  }
+}
+
+static int nk_cfg_mj(int id) {
+  switch (id) {
+#define DRN_X(id, mi, mj) \
+  case id:                \
+    return mj;
+    DRN_NK_CONFIGS(DRN_X)
+#undef DRN_X
+    default:
+      return 1;
+  }
+}
+
+static int launch_conv_nk(int id, DrnConvFwdArgs* a, hipStream_t stream) {
+  const int mi = nk_cfg_mi(id);
+  if (mi == 0 || a->K != 16 * mi || a->dil != 1 || a->bnb_x != nullptr || a->ksplit > 1 || a->sk_blocks > 0 ||
+      a->C < 8 || (a->C & (a->C - 1)) != 0 || (a->R * a->S * a->C + 31) / 32 > 9)
+    return (int)hipErrorInvalidValue;
+  if (a->in_fin.stats != nullptr && (a->N * a->P * a->Q + 16 * 4 * nk_cfg_mj(id) - 1) / (16 * 4 * nk_cfg_mj(id)) >
+                                         cfin_max_blocks()) {  // big grid: the finalize as its own launch
+    if (a->in_fin.publish) {
+      const int rc = drn_bn_fin_fwd_launch(&a->in_fin, stream);
+      if (rc) return rc;
+    }
+    DrnConvFwdArgs b = *a;
+    b.in_fin.stats = nullptr;
+    const int rc = launch_conv_nk(id, &b, stream);
+    a->tiles_p = b.tiles_p;
+    return rc;
+  }
+  const bool pro = a->in_scale != nullptr;
+  switch (id) {
+#define DRN_X(id, mi, mj) \
+  case id:                \
+    return pro ? launch_conv_nk_p<mi, mj, true>(a, stream) : launch_conv_nk_p<mi, mj, false>(a, stream);
+    DRN_NK_CONFIGS(DRN_X)
+#undef DRN_X
+    default:
+      return (int)hipErrorInvalidValue;
+  }
+}
+
+// partial-tile slots a stream-K launch needs per tile: the most workgroup ranges one tile's T
+// units touch (the kernel's owner() map, tile by tile); 0 = invalid (more workgroups than units:
+// empty ranges, or 32-bit unit arithmetic overflow)
 static int sk_slots(int tiles, int T, int G) {
   const long U = (long)tiles * T;
   if (G < 1 || T < 1 || U < G || U * (long)(G + 1) >= (1l << 31)) return 0;
-  const long L = U / G;
-  const long n = (T - 1 + L - 1) / L + 1;
-  return (int)(n < G ? n : G);
+  auto owner = [&](long u) { return ((u + 1) * G - 1) / U; };
+  long n = 1;
+  for (long t = 0; t < tiles; ++t) {
+    const long c = owner(t * T + T - 1) - owner(t * T) + 1;
+    n = c > n ? c : n;
+  }
+  return (int)n;
 }
 
 // largest grid that finalizes its input BatchNorm in the prologue (DRN_CFIN_MAX_BLOCKS)
@@ -1462,6 +1694,7 @@ DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
   if ((a->ksplit > 1 || a->sk_blocks > 0) &&
       (a->cfg < 0 || a->cfg >= DRN_GLDS_NCFG || !drn_conv_glds_ok(a) || zero == nullptr))
     return (int)hipErrorInvalidValue;  // split-K: explicit split-capable LDS-DMA configurations only
+  if (a->cfg >= DRN_NK_CFG0 && a->cfg < DRN_NK_CFG0 + DRN_NK_NCFG) return drn::launch_conv_nk(a->cfg - DRN_NK_CFG0, a, s);
   if (a->cfg >= DRN_GLDS_NCFG && a->cfg != 100) return drn_conv_mt(a->cfg - DRN_GLDS_NCFG, a, zero, s);
   if (a->bnb_x != nullptr && (!drn_conv_glds_ok(a) || zero == nullptr || a->cfg == 100))
     return (int)hipErrorInvalidValue;  // the BN-backward input transform exists on the LDS-DMA path only
@@ -1497,6 +1730,9 @@ DRN_API int drn_conv_sk_slots_cfg(const DrnConvFwdArgs* a, int cfg, int G) {
   const int bp = drn::glds_cfg_bp(cfg), bc = drn::glds_cfg_bc(cfg);
   return drn::sk_slots(((M + bp - 1) / bp) * ((a->K + bc - 1) / bc), (a->R * a->S * a->C) / bk, G);
 }
+// narrow-output (K = 16 / 32) register-operand kernels: configuration ids DRN_NK_CFG0 + i
+DRN_API int drn_conv_nk_num_cfgs() { return DRN_NK_NCFG; }
+DRN_API int drn_conv_nk_cfg0() { return DRN_NK_CFG0; }
 DRN_API int drn_conv_glds_num_cfgs() { return DRN_GLDS_NCFG + drn_conv_mt_num_cfgs(); }
 DRN_API int drn_conv_glds_default_cfg(const DrnConvFwdArgs* a) { return drn::glds_default_cfg(a); }
 

@@ -379,7 +379,12 @@ class HipBackend(_Common):
         s = self.stream()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         cands = os.environ.get("DRN_CONV_CANDS")
-        cands = [int(c) for c in cands.split(",")] if cands else [100] + list(range(self.L.drn_conv_glds_num_cfgs()))
+        if cands:
+            cands = [int(c) for c in cands.split(",")]
+        else:  # register-staged, LDS-DMA + multi-tile, narrow-output (K = 16 / 32) configurations
+            nk0 = self.L.drn_conv_nk_cfg0()
+            cands = [100] + list(range(self.L.drn_conv_glds_num_cfgs())) + \
+                [nk0 + i for i in range(self.L.drn_conv_nk_num_cfgs())] * (a.K in (16, 32))
 
         def setk(c):
             t.cfg, ks = c
@@ -464,15 +469,18 @@ class HipBackend(_Common):
     # chip, fewer write (and re-read in drn_splitk_reduce) fewer fp32 partial slabs -- the slab
     # traffic of the default 512-block target is ~1.7 GB per ResNet-50 step
     WGRAD_TARGETS = tuple(int(v) for v in os.environ.get("DRN_WGRAD_TARGETS", "128,256,384,512,768").split(","))
+    # minimum 64-pixel steps per split the tuner also tries: small layers (CIFAR stage 3 at batch
+    # 32: 32 steps) otherwise get 4 splits, i.e. 20-64 workgroups walking 8 serial steps each
+    WGRAD_MIN_STEPS_CANDS = tuple(int(v) for v in os.environ.get("DRN_WGRAD_MINSTEPS", "8,2").split(","))
 
     def wgrad_args(self, x, dy, out, g: ConvGeom, in_bn=None, relu_in=True, ws=None, target_blocks: int = 0,
-                   bnb=None, atomic: bool = False):
+                   bnb=None, atomic: bool = False, min_steps: int = 0):
         N, H, W, C = x.shape
         N2, P, Q, K = dy.shape
         Kd, R, S, Cd = out.shape
         assert Kd == K and Cd == C and N == N2
         M = N * P * Q
-        splits, pps = self.wgrad_splits(M, R * S * C, K, target_blocks)
+        splits, pps = self.wgrad_splits(M, R * S * C, K, target_blocks, min_steps)
         a = _lib.DrnConvWgradArgs()
         a.x, a.dy = x.data_ptr(), dy.data_ptr()
         a.in_scale = _ptr(in_bn[0]) if in_bn is not None else None
@@ -503,9 +511,10 @@ class HipBackend(_Common):
         """Workspace for the largest split count any candidate target can choose."""
         need = 0
         for t in set(self.WGRAD_TARGETS) | {self.WGRAD_TARGET_BLOCKS}:
-            splits, _ = self.wgrad_splits(M, R * S * C, K, t)
-            if splits > 1:
-                need = max(need, splits * K * R * S * C)
+            for ms in set(self.WGRAD_MIN_STEPS_CANDS) | {self.WGRAD_MIN_STEPS}:
+                splits, _ = self.wgrad_splits(M, R * S * C, K, t, ms)
+                if splits > 1:
+                    need = max(need, splits * K * R * S * C)
         return need
 
     @staticmethod
@@ -529,12 +538,13 @@ class HipBackend(_Common):
         real launch that follows)."""
         st = self.stream()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        best, best_t = (0, 2, False), float("inf")
+        best, best_t = (0, 2, False, 0), float("inf")
         cands = tuple(int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6,7,8").split(","))
         seen = set()
         modes = (False, True) if self.wgrad_atomic_ok else (False,)
-        for tgt, atomic in [(t, m) for t in self.WGRAD_TARGETS for m in modes]:
-            a = args_for(tgt, atomic)
+        for tgt, atomic, ms_min in [(t, m, k) for t in self.WGRAD_TARGETS for m in modes
+                                for k in self.WGRAD_MIN_STEPS_CANDS]:
+            a = args_for(tgt, atomic, ms_min)
             if (a.splits, a.atomic_out) in seen:
                 continue
             seen.add((a.splits, a.atomic_out))
@@ -548,16 +558,17 @@ class HipBackend(_Common):
                     self._wgrad_full(a, ns, out, st)
                 ev1.record()
                 ev1.synchronize()
-                ms = ev0.elapsed_time(ev1) / iters
-                if ms < best_t:
-                    best, best_t = (tgt, ns, bool(a.atomic_out)), ms
+                t_ms = ev0.elapsed_time(ev1) / iters
+                if t_ms < best_t:
+                    best, best_t = (tgt, ns, bool(a.atomic_out), ms_min), t_ms
         if best[2]:
             self.wgrad_atomic_used = True  # the executor now zeroes the gradients every step
         self.tune_log.append((("wgrad",) + key, best, round(best_t * 1e3, 1)))
         return best
 
     def conv_wgrad(self, x, dy, out, g, in_bn=None, relu_in=True, ws=None, bnb=None):
-        args_for = lambda tgt, atomic=False: self.wgrad_args(x, dy, out, g, in_bn, relu_in, ws, tgt, bnb, atomic)
+        args_for = lambda tgt, atomic=False, ms=0: self.wgrad_args(x, dy, out, g, in_bn, relu_in, ws, tgt, bnb, atomic,
+                                                                   ms)
         a = args_for(0)
         st = self.stream()
         if self.forced_wgrad_ns is not None:
@@ -568,11 +579,11 @@ class HipBackend(_Common):
             self.wgrad_ns[key] = self._tune_wgrad(args_for, out, key)
             if self.wgrad_ns[key][2]:
                 self.zero_(out)  # the timing launches left partial sums in this gradient slot
-        tgt, ns, atomic = self.wgrad_ns.get(key, (0, 2, False))
+        tgt, ns, atomic, ms = self.wgrad_ns.get(key, (0, 2, False, 0))
         if ns == 0 and a.bnb_x is not None:
             ns = 2
-        if tgt or atomic:
-            a = args_for(tgt, atomic)
+        if tgt or atomic or ms:
+            a = args_for(tgt, atomic, ms)
         self._wgrad_full(a, ns, out, st)
 
     # -- batch norm -----------------------------------------------------------------------------

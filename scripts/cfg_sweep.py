@@ -40,7 +40,8 @@ if "res" in flags:
 if "stats" in flags:
     kw["stats"] = torch.zeros(8, 2, K, device="cuda")
 out = []
-for cfg in [100] + list(range(be.L.drn_conv_glds_num_cfgs())):
+nk = [be.L.drn_conv_nk_cfg0() + i for i in range(be.L.drn_conv_nk_num_cfgs())] if K in (16, 32) else []
+for cfg in [100] + list(range(be.L.drn_conv_glds_num_cfgs())) + nk:
     # split-K factors / stream-K grids (< 0; only the split-capable configurations accept them)
     for ks in (1, 2, 3, 4, -256, -512):
         a = be.conv_args(x, w, y, g, **kw)
