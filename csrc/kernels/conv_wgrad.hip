@@ -29,6 +29,18 @@
 
 namespace drn {
 
+// Per-workgroup timeline of the LDS-DMA weight-gradient kernel, compiled in only with
+// -DDRN_CONV_TRACE (the diagnostics build, as for the forward conv): b = {start, main-loop end,
+// end} in s_memrealtime ticks (100 MHz) + HW_ID / XCC_ID, at the workgroup's linear launch index.
+#ifdef DRN_CONV_TRACE
+__device__ unsigned long long* g_wgrad_trace = nullptr;
+__device__ __forceinline__ unsigned long long wg_realtime() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
+  return t;
+}
+#endif
+
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, const DrnFastDiv& f) { return drn_fdiv(n, f); }
 
 // 32-byte-slot swizzle for rows of W bytes (W = 128 or 256)
@@ -370,6 +382,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
   static_assert(IA >= 1 && IB >= 1 && NS >= 2, "geometry");
 
   extern __shared__ __attribute__((aligned(1024))) char smem[];
+#ifdef DRN_CONV_TRACE
+  unsigned long long* const trace = g_wgrad_trace;
+  unsigned long long t_start = 0;
+  if (trace != nullptr) t_start = wg_realtime();
+#endif
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int Ktot = a.R * a.S * a.C;
@@ -705,7 +722,26 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
     asm volatile("" ::: "memory");
   }
 
+#ifdef DRN_CONV_TRACE
+  unsigned long long t_loop = 0;
+  if (trace != nullptr) t_loop = wg_realtime();
+#endif
   wgrad_store<MI, MJ>(a, acc, split, c0 + wc * WCO, k0 + wk * WKK, Ktot, lane);
+#ifdef DRN_CONV_TRACE
+  if (trace != nullptr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+      const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+      unsigned long long* r = trace + 4 * (size_t)(blockIdx.x + blockIdx.y * gridDim.x);
+      r[0] = t_start;
+      r[1] = t_loop;
+      r[2] = wg_realtime();
+      r[3] = ((unsigned long long)xcc << 32) | hw;
+    }
+  }
+#endif
 }
 
 template <int BKK, int BCO, int NS, int BP, bool PRO, bool BNB = false, bool IL = false>
@@ -822,6 +858,13 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 }  // namespace drn
 
 // Block-tile shape the dispatcher picks (host mirror used to size the split-K grid).
+#ifdef DRN_CONV_TRACE
+// diagnostics: per-workgroup timeline buffer for the LDS-DMA weight-gradient kernel
+DRN_API int drn_wgrad_trace_set(unsigned long long* buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(drn::g_wgrad_trace), &buf, sizeof(buf));
+}
+#endif
+
 DRN_API int drn_wgrad_tiles(int Ktot, int K) {
   const int bkk = Ktot > 64 ? 128 : 64, bco = K > 64 ? 128 : 64;
   return ((Ktot + bkk - 1) / bkk) * ((K + bco - 1) / bco);

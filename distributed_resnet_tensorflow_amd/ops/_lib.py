@@ -18,7 +18,7 @@ _LIB = None
 _LOCK = threading.Lock()
 LIB_PATH = Path(os.environ.get("DRN_KERNEL_LIB") or Path(__file__).resolve().parent / "libdrn_kernels.so")
 # diagnostics-only entry points an older library (A/B runs via DRN_KERNEL_LIB) may lack
-_OPTIONAL = {"drn_conv_trace_set"}  # a -DDRN_CONV_TRACE build only
+_OPTIONAL = {"drn_conv_trace_set", "drn_wgrad_trace_set"}  # a -DDRN_CONV_TRACE build only
 
 c_int = ctypes.c_int
 c_i64 = ctypes.c_int64
@@ -86,6 +86,7 @@ _SIGS = {
     "drn_conv_glds_ok": ([ctypes.POINTER(DrnConvFwdArgs)], c_int),
     "drn_conv_glds_num_cfgs": ([], c_int),
     "drn_conv_trace_set": ([c_p], c_int),
+    "drn_wgrad_trace_set": ([c_p], c_int),
     "drn_conv_glds_default_cfg": ([ctypes.POINTER(DrnConvFwdArgs)], c_int),
     "drn_conv_wgrad": ([ctypes.POINTER(DrnConvWgradArgs), c_p], c_int),
     "drn_conv_wgrad2": ([ctypes.POINTER(DrnConvWgradArgs), c_p, c_int, c_p], c_int),

@@ -404,6 +404,8 @@ class Executor:
             x, x_stats, x_G = self.stem_out, self.stem_stats, self.stem_G
         self.blocks: List[BlockPlan] = []
         ws_need = be.wgrad_ws_elems(N * hs * hs, sp.stem.cout, sp.stem.k, sp.stem.k, sp.stem.cin_store)
+        if self.stem_pack:  # the packed stem's gradient has fewer k-tiles, so it may take more splits
+            ws_need = max(ws_need, be.wgrad_ws_elems(N * hs * hs, *self.stem_dw4.shape))
         for blk in sp.blocks:
             bns = [self._bn_state(blk.bn1)] + [self._bn_state(b) for b in blk.bns]
             bns[0].stats, bns[0].G = x_stats, x_G
