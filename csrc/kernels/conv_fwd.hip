@@ -694,7 +694,7 @@ __device__ __forceinline__ void conv_fwd_glds_tile(const DrnConvFwdArgs& a, cons
 #endif
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably uniform: LDS-DMA destinations stay scalar
   const int M = a.N * a.P * a.Q;
   const int C = a.C;
   const int Ktot = a.R * a.S * C;
@@ -741,6 +741,24 @@ __device__ __forceinline__ void conv_fwd_glds_tile(const DrnConvFwdArgs& a, cons
       boff[i] = 0;
     }
   }
+  // Uniform-base fast path (cf. conv_wgrad.hip: per-piece address arithmetic, not the matrix
+  // pipe, bounded the main loop): for a 1x1 unpadded convolution every B row of a tile that lies
+  // wholly inside the output is a valid pixel for the whole reduction, and with a full channel
+  // tile every A row is a real filter -- such stages issue each piece as a wave-uniform stage base
+  // plus a per-lane offset fixed for the whole kernel, with no per-lane test.
+#ifndef DRN_NO_FAST_LOADER  // (-DDRN_NO_FAST_LOADER: the per-lane path everywhere, for A/B variant builds)
+  const bool fast_b = !SROW && !BNB && a.R == 1 && a.S == 1 && a.pad_h == 0 && a.pad_w == 0 && m0 + BP <= M;
+  const bool fast_a = !SROW && c0 + BC <= a.K;
+#else
+  const bool fast_b = false, fast_a = false;
+#endif
+  uint32_t aoff_w[GA], boff_x[GB];
+#pragma unroll
+  for (int i = 0; i < GA; ++i)
+    aoff_w[i] = (uint32_t)((RPG * NW * i + RPG * wave + lrow) * Ktot + (lpc ^ glds_swz<BK>(RPG * NW * i + RPG * wave + lrow)) * 8);
+#pragma unroll
+  for (int i = 0; i < GB; ++i) boff_x[i] = (uint32_t)boff[i];
+  const bf16_t* __restrict__ w0 = reinterpret_cast<const bf16_t*>(a.w) + (size_t)c0 * Ktot;
   // wave-uniform k iterator of the next stage to issue: k offset, tap (r, s), channel offset
   int ik = 0, ir = 0, is = 0, ici = 0;
   int t_beg = 0, t_cnt = 0;  // KS: this split's / stream-K segment's k-stage range
@@ -779,18 +797,30 @@ __device__ __forceinline__ void conv_fwd_glds_tile(const DrnConvFwdArgs& a, cons
       ++ir;
       return;
     }
+    if (fast_a) {
+      const bf16_t* __restrict__ ws_ = w0 + ik;
 #pragma unroll
-    for (int i = 0; i < GA; ++i) {
-      const void* src = wsrc[i] ? (const void*)(wsrc[i] + ik) : zero;
-      glds16(src, st + (RPG * NW * i + RPG * wave) * ROWB);
+      for (int i = 0; i < GA; ++i) glds16(ws_ + aoff_w[i], st + (RPG * NW * i + RPG * wave) * ROWB);
+    } else {
+#pragma unroll
+      for (int i = 0; i < GA; ++i) {
+        const void* src = wsrc[i] ? (const void*)(wsrc[i] + ik) : zero;
+        glds16(src, st + (RPG * NW * i + RPG * wave) * ROWB);
+      }
     }
     const int tap_off = (ir * a.W + is) * C + ici;
+    if (fast_b) {
+      const bf16_t* __restrict__ xs_ = xg + tap_off;
 #pragma unroll
-    for (int i = 0; i < GB; ++i) {
-      const int h = bh[i] + ir, w = bw[i] + is;
-      const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-      const void* src = ok ? (const void*)(xg + (boff[i] + tap_off)) : zero;
-      glds16(src, st + (BC + RPG * NW * i + RPG * wave) * ROWB);
+      for (int i = 0; i < GB; ++i) glds16(xs_ + boff_x[i], st + (BC + RPG * NW * i + RPG * wave) * ROWB);
+    } else {
+#pragma unroll
+      for (int i = 0; i < GB; ++i) {
+        const int h = bh[i] + ir, w = bw[i] + is;
+        const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+        const void* src = ok ? (const void*)(xg + (boff[i] + tap_off)) : zero;
+        glds16(src, st + (BC + RPG * NW * i + RPG * wave) * ROWB);
+      }
     }
     if constexpr (BNB) {  // the BatchNorm input pieces at the same positions
       const bf16_t* __restrict__ bx = reinterpret_cast<const bf16_t*>(a.bnb_x);

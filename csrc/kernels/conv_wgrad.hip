@@ -22,6 +22,7 @@
 // drn_splitk_reduce (no float atomics: bitwise-reproducible weight gradients).
 #include "drn_common.h"
 #include "drn_conv.h"
+#include <stdlib.h>
 
 #ifndef DRN_WGRAD_STAGES
 #define DRN_WGRAD_STAGES 2
@@ -42,6 +43,12 @@ __device__ __forceinline__ unsigned long long wg_realtime() {
 #endif
 
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, const DrnFastDiv& f) { return drn_fdiv(n, f); }
+
+// A/B switch read once per process (e.g. DRN_WGRAD_LIN=0 restores the generic patch loader)
+static bool getenv_flag(const char* name, bool dflt) {
+  const char* e = getenv(name);
+  return e == nullptr ? dflt : atoi(e) != 0;
+}
 
 // 32-byte-slot swizzle for rows of W bytes (W = 128 or 256)
 template <int W>
@@ -365,7 +372,18 @@ __device__ __forceinline__ void lgkm_fence(s16x4v (&a)[MI][2], s16x4v (&b)[MJ][2
 // IL: the next stage's LDS-DMA pieces are issued one at a time between this stage's MFMAs
 // (instead of all right after the barrier, where every wave issues in lockstep and the matrix
 // pipe idles for the DMA issue time).
-template <int BKK, int BCO, int NS, int BP = 64, bool PRO = false, bool BNB = false, bool IL = false>
+//
+// Loader address arithmetic (measured per-workgroup timelines, profiles/r3_wgrad_timelines.txt:
+// 1.4 us per 64-pixel step at 2 workgroups/CU, i.e. ~35 % of the MFMA rate; the main loop issued
+// ~170 VALU/SALU instructions per wave and step for 32 MFMAs, most of them the per-piece pixel
+// decode and zero-page selects): every source address is a WAVE-UNIFORM stage base (SGPRs) plus a
+// per-lane offset fixed for the whole kernel, and a stage whose pieces are all in range (every
+// stage but a split's partial last one, when the tile's channel ranges are full) issues with no
+// per-lane test at all.
+// LIN: 1x1 stride-1 unpadded convolutions (33 of ResNet-50's 53 weight gradients): the patch row
+// of pixel m is x[m][k0..] itself, so the patch loader is as cheap as the dY loader (no pixel
+// decode, no padding test).
+template <int BKK, int BCO, int NS, int BP = 64, bool PRO = false, bool BNB = false, bool IL = false, bool LIN = false>
 __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a, const void* __restrict__ zero) {
   static_assert(BP == 32 || BP == 64, "pixels per stage");
   constexpr int KS = BP / 32;  // 32-deep MFMA k-slices per stage
@@ -388,7 +406,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
   if (trace != nullptr) t_start = wg_realtime();
 #endif
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // (wave index made provably wave-uniform: LDS-DMA destinations then stay in SGPRs / M0)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int Ktot = a.R * a.S * a.C;
   const int M = a.N * a.P * a.Q;
   const int nkt = (Ktot + BKK - 1) / BKK;
@@ -457,6 +476,19 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
   const bf16_t* __restrict__ xg = reinterpret_cast<const bf16_t*>(a.x);
   const bf16_t* __restrict__ dyg = reinterpret_cast<const bf16_t*>(a.dy) + dc;
   const bf16_t* __restrict__ bxg = BNB ? reinterpret_cast<const bf16_t*>(a.bnb_x) + dc : nullptr;
+  static_assert(!(LIN && IL), "LIN: plain stage issue only");
+  // uniform fast-path conditions (every lane's k / output-channel chunk in range) and the per-lane
+  // element offsets of the pieces inside a stage (stage base = uniform pixel offset)
+  const bool a_full = k0 + BKK <= Ktot, b_full = c0 + BCO <= a.K;
+  const bf16_t* __restrict__ dy0 = reinterpret_cast<const bf16_t*>(a.dy);
+  const bf16_t* __restrict__ bx0 = BNB ? reinterpret_cast<const bf16_t*>(a.bnb_x) : nullptr;
+  uint32_t offB[IB], offA[LIN ? IA : 1];
+#pragma unroll
+  for (int i = 0; i < IB; ++i) offB[i] = (uint32_t)((RIB * (wave + 4 * i) + brow) * a.K + dc);
+  if constexpr (LIN) {
+#pragma unroll
+    for (int i = 0; i < IA; ++i) offA[i] = (uint32_t)((RIA * (wave + 4 * i) + arow) * a.C + kk);
+  }
   float bA[8], bB[8], bD[8];  // BNB: this lane's 8 dY channels' coefficients
   if constexpr (BNB) {
     // finalize the block's BCO channels into LDS (behind the pipeline stages), then each lane
@@ -498,49 +530,106 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
     ap[i] = (int)p;
     aq[i] = (int)(rem - p * (uint32_t)a.Q);
   }
+  // Generic patch loader state, advanced incrementally (no multiplies in the loop): the input row
+  // / column of the lane's tap (hh, ww) and the element offset po of (n, hh, ww, ci); the q wrap is
+  // a select, p wraps (an image boundary inside the 64-pixel step) a short loop.
+  int hh[IA], ww[IA], po[IA];
+#pragma unroll
+  for (int i = 0; i < IA; ++i) {
+    hh[i] = ap[i] * a.stride + roff;
+    ww[i] = aq[i] * a.stride + soff;
+    po[i] = (an[i] * a.H + hh[i]) * WC + ww[i] * a.C + ci;
+  }
+  const int Qs = a.Q * a.stride, Ps = a.P * a.stride;
+  const int w_lim = Qs + soff, h_lim = Ps + roff;
+  const int d_w = dq * a.stride, d_h = dp * a.stride;
+  const int d_po = d_h * WC + d_w * a.C;               // plain step
+  const int wrap_q = a.stride * WC - Qs * a.C;         // q wrapped: next input row band
+  const int wrap_p = HWC - Ps * WC;                     // p wrapped: next image
 
   auto issue = [&](int slot, int mstep) {
     char* st = smem + slot * STAGE;
+#ifndef DRN_NO_FAST_LOADER
+    const bool full = mstep + BP <= mend;  // wave-uniform: no piece of this stage is past the split
+#else
+    const bool full = false;
+#endif
+    if constexpr (LIN) {
+      const bf16_t* __restrict__ xs = xg + (size_t)mstep * a.C;
+      if (full && a_full) {
 #pragma unroll
-    for (int i = 0; i < IA; ++i) {
+        for (int i = 0; i < IA; ++i)
+          __builtin_amdgcn_global_load_lds((wg_gbl_void*)(xs + offA[i]), (wg_lds_void*)(st + RIA * (wave + 4 * i) * WA),
+                                           16, 0, 0);
+        if constexpr (PRO) okm |= ((1u << IA) - 1u) << (slot * IA);
+      } else {
+#pragma unroll
+        for (int i = 0; i < IA; ++i) {
+          const bool ok = kvalid && mstep + RIA * (wave + 4 * i) + arow < mend;
+          if constexpr (PRO) {
+            const uint32_t bit = 1u << (slot * IA + i);
+            okm = ok ? (okm | bit) : (okm & ~bit);
+          }
+          __builtin_amdgcn_global_load_lds((wg_gbl_void*)(ok ? (const void*)(xs + offA[i]) : zero),
+                                           (wg_lds_void*)(st + RIA * (wave + 4 * i) * WA), 16, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < (LIN ? 0 : IA); ++i) {
       const int r0 = RIA * (wave + 4 * i);
-      const int h = __mul24(ap[i], a.stride) + roff;
-      const int w = __mul24(aq[i], a.stride) + soff;
-      const bool ok = kvalid && am[i] < mend && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-      const uint32_t off = (uint32_t)(__mul24(an[i], HWC) + __mul24(h, WC) + __mul24(w, a.C) + ci);
-      const void* src = ok ? (const void*)(xg + off) : zero;
+      // (bitwise, not short-circuit: one select per piece instead of exec-mask branches)
+      const bool ok = kvalid & (full | (am[i] < mend)) & ((unsigned)hh[i] < (unsigned)a.H) &
+                      ((unsigned)ww[i] < (unsigned)a.W);
+      const bf16_t* const pa = xg + (uint32_t)po[i];
+      const void* src = ok ? (const void*)pa : zero;
       if constexpr (PRO) {
         const uint32_t bit = 1u << (slot * IA + i);
         okm = ok ? (okm | bit) : (okm & ~bit);
       }
       __builtin_amdgcn_global_load_lds((wg_gbl_void*)src, (wg_lds_void*)(st + r0 * WA), 16, 0, 0);
       am[i] += BP;
-      aq[i] += dq;
-      ap[i] += dp;
-      if (aq[i] >= a.Q) {
-        aq[i] -= a.Q;
-        ++ap[i];
-      }
-      while (ap[i] >= a.P) {
-        ap[i] -= a.P;
-        ++an[i];
+      ww[i] += d_w;
+      hh[i] += d_h;
+      po[i] += d_po;
+      const bool wq = ww[i] >= w_lim;
+      ww[i] = wq ? ww[i] - Qs : ww[i];
+      hh[i] = wq ? hh[i] + a.stride : hh[i];
+      po[i] += wq ? wrap_q : 0;
+      while (hh[i] >= h_lim) {
+        hh[i] -= Ps;
+        po[i] += wrap_p;
       }
     }
+    const bf16_t* __restrict__ ds = dy0 + (size_t)mstep * a.K;
+    const bf16_t* __restrict__ xbs = BNB ? bx0 + (size_t)mstep * a.K : nullptr;
+    if (full && b_full) {
 #pragma unroll
-    for (int i = 0; i < IB; ++i) {
-      const int r0 = RIB * (wave + 4 * i);
-      const int m = mstep + r0 + brow;
-      const void* src = (cvalid && m < mend) ? (const void*)(dyg + (uint32_t)__mul24(m, a.K)) : zero;
-      __builtin_amdgcn_global_load_lds((wg_gbl_void*)src, (wg_lds_void*)(st + A_BYTES + r0 * WB), 16, 0, 0);
-    }
-    if constexpr (BNB) {
+      for (int i = 0; i < IB; ++i)
+        __builtin_amdgcn_global_load_lds((wg_gbl_void*)(ds + offB[i]), (wg_lds_void*)(st + A_BYTES + RIB * (wave + 4 * i) * WB),
+                                         16, 0, 0);
+      if constexpr (BNB) {
+#pragma unroll
+        for (int i = 0; i < IB; ++i)
+          __builtin_amdgcn_global_load_lds((wg_gbl_void*)(xbs + offB[i]),
+                                           (wg_lds_void*)(st + A_BYTES + BP * WB + RIB * (wave + 4 * i) * WB), 16, 0, 0);
+      }
+    } else {
 #pragma unroll
       for (int i = 0; i < IB; ++i) {
         const int r0 = RIB * (wave + 4 * i);
-        const int m = mstep + r0 + brow;
-        const void* src = (cvalid && m < mend) ? (const void*)(bxg + (uint32_t)__mul24(m, a.K)) : zero;
-        __builtin_amdgcn_global_load_lds((wg_gbl_void*)src, (wg_lds_void*)(st + A_BYTES + BP * WB + r0 * WB), 16,
-                                         0, 0);
+        const bool ok = cvalid && mstep + r0 + brow < mend;
+        __builtin_amdgcn_global_load_lds((wg_gbl_void*)(ok ? (const void*)(ds + offB[i]) : zero),
+                                         (wg_lds_void*)(st + A_BYTES + r0 * WB), 16, 0, 0);
+      }
+      if constexpr (BNB) {
+#pragma unroll
+        for (int i = 0; i < IB; ++i) {
+          const int r0 = RIB * (wave + 4 * i);
+          const bool ok = cvalid && mstep + r0 + brow < mend;
+          __builtin_amdgcn_global_load_lds((wg_gbl_void*)(ok ? (const void*)(xbs + offB[i]) : zero),
+                                           (wg_lds_void*)(st + A_BYTES + BP * WB + r0 * WB), 16, 0, 0);
+        }
       }
     }
   };
@@ -744,11 +833,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
 #endif
 }
 
-template <int BKK, int BCO, int NS, int BP, bool PRO, bool BNB = false, bool IL = false>
+template <int BKK, int BCO, int NS, int BP, bool PRO, bool BNB = false, bool IL = false, bool LIN = false>
 static int launch_wgrad_glds_p(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
   constexpr int LDS = NS * (BP * BKK * 2 + BP * BCO * 2 * (BNB ? 2 : 1)) + (BNB ? 12 * BCO : 0);
   static bool attr_set = false;
-  auto kern = conv_wgrad_glds_kernel<BKK, BCO, NS, BP, PRO, BNB, IL>;
+  auto kern = conv_wgrad_glds_kernel<BKK, BCO, NS, BP, PRO, BNB, IL, LIN>;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
@@ -762,6 +851,23 @@ static int launch_wgrad_glds_p(DrnConvWgradArgs* a, const void* zero, hipStream_
 
 template <int BKK, int BCO, int NS, int BP = 64, bool IL = false>
 static int launch_wgrad_glds(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
+#ifndef DRN_NO_FAST_LOADER
+  static const bool lin_on = getenv_flag("DRN_WGRAD_LIN", true);
+#else
+  static const bool lin_on = false;
+#endif
+  const bool lin = !IL && lin_on && a->R == 1 && a->S == 1 && a->stride == 1 && a->pad_h == 0 && a->pad_w == 0 &&
+                   a->C % 8 == 0;
+  if constexpr (!IL) {
+    if (lin) {
+      if (a->bnb_x != nullptr) {
+        if (a->in_scale != nullptr) return launch_wgrad_glds_p<BKK, BCO, NS, BP, true, true, false, true>(a, zero, s);
+        return launch_wgrad_glds_p<BKK, BCO, NS, BP, false, true, false, true>(a, zero, s);
+      }
+      if (a->in_scale != nullptr) return launch_wgrad_glds_p<BKK, BCO, NS, BP, true, false, false, true>(a, zero, s);
+      return launch_wgrad_glds_p<BKK, BCO, NS, BP, false, false, false, true>(a, zero, s);
+    }
+  }
   if (a->bnb_x != nullptr) {
     if (a->in_scale != nullptr) return launch_wgrad_glds_p<BKK, BCO, NS, BP, true, true, IL>(a, zero, s);
     return launch_wgrad_glds_p<BKK, BCO, NS, BP, false, true, IL>(a, zero, s);
@@ -857,7 +963,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
 
 }  // namespace drn
 
-// Block-tile shape the dispatcher picks (host mirror used to size the split-K grid).
 #ifdef DRN_CONV_TRACE
 // diagnostics: per-workgroup timeline buffer for the LDS-DMA weight-gradient kernel
 DRN_API int drn_wgrad_trace_set(unsigned long long* buf) {
@@ -865,6 +970,7 @@ DRN_API int drn_wgrad_trace_set(unsigned long long* buf) {
 }
 #endif
 
+// Block-tile shape the dispatcher picks (host mirror used to size the split-K grid).
 DRN_API int drn_wgrad_tiles(int Ktot, int K) {
   const int bkk = Ktot > 64 ? 128 : 64, bco = K > 64 ? 128 : 64;
   return ((Ktot + bkk - 1) / bkk) * ((K + bco - 1) / bco);

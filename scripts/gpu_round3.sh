@@ -5,7 +5,7 @@
 OUT=${1:-gpurun_out/r3}
 export PYTHONPATH=$(pwd)
 mkdir -p "$OUT"
-timeout -k 10 1000 python -u -m pytest tests -m gpu --maxfail=5 -q --timeout 170 --timeout-method thread \
+timeout -k 10 1000 python -u -m pytest ${TESTS:-tests} -m gpu --maxfail=5 -q --timeout 170 --timeout-method thread \
   > "$OUT/gputests.log" 2>&1
 rc=$?
 tail -3 "$OUT/gputests.log"

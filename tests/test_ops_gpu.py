@@ -475,6 +475,9 @@ WGRAD_GLDS_CASES = [
     (2, 16, 16, 8, 64, 7, 2, 3),      # stem: Ktot = 392 (partial k tile)
     (2, 7, 7, 256, 72, 3, 1, 1),      # K % BCO != 0
     (1, 6, 6, 32, 16, 3, 1, 1),       # narrow (64 x 64 tiles)
+    (3, 7, 7, 128, 256, 1, 1, 0),     # 1x1 stride-1 (uniform-base loader): 147 pixels, partial last stage
+    (2, 9, 9, 72, 200, 1, 1, 0),      # 1x1 stride-1, partial k and output-channel tiles
+    (8, 14, 14, 256, 128, 1, 1, 0),   # 1x1 stride-1, several pixel splits
 ]
 
 

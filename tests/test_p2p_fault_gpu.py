@@ -34,6 +34,13 @@ def _free_port():
     return p
 
 
+def _flush(q):
+    """Queue.put hands the item to a feeder thread; os._exit right after it can kill the process
+    before the item reaches the pipe, so close the queue and join that thread first."""
+    q.close()
+    q.join_thread()
+
+
 def _worker(rank, mode, port, ck, q, stop):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DRN_P2P_TIMEOUT_MS="1000")
     import torch.distributed as dist
@@ -86,10 +93,12 @@ def _worker(rank, mode, port, ck, q, stop):
         same = torch.equal(w0, sess.ex.P.master) and torch.equal(m0, sess.ex.P.momentum)
         later = sorted(f for f in os.listdir(ck) if f.startswith("model.ckpt-") and not f.startswith("model.ckpt-2."))
         q.put((0, (err, dt, same, later, sess.failed)))
+        _flush(q)
         os._exit(1 if err else 0)
     except Exception as e:  # pragma: no cover
         import traceback
         q.put((rank, repr(e) + traceback.format_exc()))
+        _flush(q)
         os._exit(2)
 
 
