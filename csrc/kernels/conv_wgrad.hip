@@ -547,6 +547,60 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
   const int wrap_q = a.stride * WC - Qs * a.C;         // q wrapped: next input row band
   const int wrap_p = HWC - Ps * WC;                     // p wrapped: next image
 
+  // one generic patch piece i of a stage (slot st): load, then advance the lane's pixel state by
+  // one 64-pixel step (shared by issue() and the interleaved issue_piece())
+  auto a_piece = [&](char* st, int slot, int i, bool full) {
+    const int r0 = RIA * (wave + 4 * i);
+#ifdef DRN_WGRAD_GENERIC_DECODE  // A/B: the per-step pixel decode of the previous revision
+    {
+      const int h = __mul24(ap[i], a.stride) + roff;
+      const int w = __mul24(aq[i], a.stride) + soff;
+      const bool ok = kvalid && am[i] < mend && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+      const uint32_t off = (uint32_t)(__mul24(an[i], HWC) + __mul24(h, WC) + __mul24(w, a.C) + ci);
+      const void* src = ok ? (const void*)(xg + off) : zero;
+      if constexpr (PRO) {
+        const uint32_t bit = 1u << (slot * IA + i);
+        okm = ok ? (okm | bit) : (okm & ~bit);
+      }
+      __builtin_amdgcn_global_load_lds((wg_gbl_void*)src, (wg_lds_void*)(st + r0 * WA), 16, 0, 0);
+      am[i] += BP;
+      aq[i] += dq;
+      ap[i] += dp;
+      if (aq[i] >= a.Q) {
+        aq[i] -= a.Q;
+        ++ap[i];
+      }
+      while (ap[i] >= a.P) {
+        ap[i] -= a.P;
+        ++an[i];
+      }
+      return;
+    }
+#endif
+    // (bitwise, not short-circuit: one select per piece instead of exec-mask branches)
+    const bool ok = kvalid & (full | (am[i] < mend)) & ((unsigned)hh[i] < (unsigned)a.H) &
+                    ((unsigned)ww[i] < (unsigned)a.W);
+    const bf16_t* const pa = xg + (uint32_t)po[i];
+    const void* src = ok ? (const void*)pa : zero;
+    if constexpr (PRO) {
+      const uint32_t bit = 1u << (slot * IA + i);
+      okm = ok ? (okm | bit) : (okm & ~bit);
+    }
+    __builtin_amdgcn_global_load_lds((wg_gbl_void*)src, (wg_lds_void*)(st + r0 * WA), 16, 0, 0);
+    am[i] += BP;
+    ww[i] += d_w;
+    hh[i] += d_h;
+    po[i] += d_po;
+    const bool wq = ww[i] >= w_lim;
+    ww[i] = wq ? ww[i] - Qs : ww[i];
+    hh[i] = wq ? hh[i] + a.stride : hh[i];
+    po[i] += wq ? wrap_q : 0;
+    while (hh[i] >= h_lim) {
+      hh[i] -= Ps;
+      po[i] += wrap_p;
+    }
+  };
+
   auto issue = [&](int slot, int mstep) {
     char* st = smem + slot * STAGE;
 #ifndef DRN_NO_FAST_LOADER
@@ -576,31 +630,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
       }
     }
 #pragma unroll
-    for (int i = 0; i < (LIN ? 0 : IA); ++i) {
-      const int r0 = RIA * (wave + 4 * i);
-      // (bitwise, not short-circuit: one select per piece instead of exec-mask branches)
-      const bool ok = kvalid & (full | (am[i] < mend)) & ((unsigned)hh[i] < (unsigned)a.H) &
-                      ((unsigned)ww[i] < (unsigned)a.W);
-      const bf16_t* const pa = xg + (uint32_t)po[i];
-      const void* src = ok ? (const void*)pa : zero;
-      if constexpr (PRO) {
-        const uint32_t bit = 1u << (slot * IA + i);
-        okm = ok ? (okm | bit) : (okm & ~bit);
-      }
-      __builtin_amdgcn_global_load_lds((wg_gbl_void*)src, (wg_lds_void*)(st + r0 * WA), 16, 0, 0);
-      am[i] += BP;
-      ww[i] += d_w;
-      hh[i] += d_h;
-      po[i] += d_po;
-      const bool wq = ww[i] >= w_lim;
-      ww[i] = wq ? ww[i] - Qs : ww[i];
-      hh[i] = wq ? hh[i] + a.stride : hh[i];
-      po[i] += wq ? wrap_q : 0;
-      while (hh[i] >= h_lim) {
-        hh[i] -= Ps;
-        po[i] += wrap_p;
-      }
-    }
+    for (int i = 0; i < (LIN ? 0 : IA); ++i) a_piece(st, slot, i, full);
     const bf16_t* __restrict__ ds = dy0 + (size_t)mstep * a.K;
     const bf16_t* __restrict__ xbs = BNB ? bx0 + (size_t)mstep * a.K : nullptr;
     if (full && b_full) {
@@ -639,29 +669,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
   auto issue_piece = [&](int slot, int mstep, int gp) {
     char* st = smem + slot * STAGE;
     if (gp < IA) {
-      const int i = gp;
-      const int r0 = RIA * (wave + 4 * i);
-      const int h = __mul24(ap[i], a.stride) + roff;
-      const int w = __mul24(aq[i], a.stride) + soff;
-      const bool ok = kvalid && am[i] < mend && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-      const uint32_t off = (uint32_t)(__mul24(an[i], HWC) + __mul24(h, WC) + __mul24(w, a.C) + ci);
-      if constexpr (PRO) {
-        const uint32_t bit = 1u << (slot * IA + i);
-        okm = ok ? (okm | bit) : (okm & ~bit);
-      }
-      __builtin_amdgcn_global_load_lds((wg_gbl_void*)(ok ? (const void*)(xg + off) : zero),
-                                       (wg_lds_void*)(st + r0 * WA), 16, 0, 0);
-      am[i] += BP;
-      aq[i] += dq;
-      ap[i] += dp;
-      if (aq[i] >= a.Q) {
-        aq[i] -= a.Q;
-        ++ap[i];
-      }
-      while (ap[i] >= a.P) {
-        ap[i] -= a.P;
-        ++an[i];
-      }
+      a_piece(st, slot, gp, false);
       return;
     }
     const int i = (gp - IA) % IB;
