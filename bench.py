@@ -79,11 +79,19 @@ def main():
     p2p = (world > 1 or force_dp) and p2p_wanted(args.allreduce, spec.num_params() * 4, world,
                                                  shard_optimizer=bool(args.shard_optimizer))
     eager_dp = (world > 1 or force_dp) and not p2p
+    prio = None
     if (eager_dp or args.graph == 0) and args.graph != 1:
         # eager data-parallel step: its main (critical-path) stream at HIGH priority -- see
         # parallel.engine.use_priority_main_stream
         from distributed_resnet_tensorflow_amd.parallel.engine import use_priority_main_stream
         use_priority_main_stream()
+    elif args.graph == -1 and not (world > 1 or force_dp):
+        # auto on one GPU: the EAGER candidate runs on a high-priority main stream too (ResNet-50
+        # bs128, one box: 9.92-9.94 ms vs 10.15-10.19 ms on the normal-priority stream,
+        # profiles/r3_side_stream_ab.txt); the HIP-graph candidate is captured and replayed from
+        # a normal-priority stream (replay from a high-priority one measured far slower)
+        from distributed_resnet_tensorflow_amd.parallel.engine import make_priority_stream
+        prio = make_priority_stream()
     if world > 1 or force_dp:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -118,6 +126,12 @@ def main():
             eng.apply_gradients(eng.finish(), 1.0 / world)
         else:
             ex.apply_gradients()
+
+    eager = step
+    if prio is not None:
+        def eager():
+            with torch.cuda.stream(prio):
+                step()
 
     # kernel autotuning pass (one plain forward + backward) before any collective is in flight,
     # so every rank times its candidate kernels on an otherwise idle GPU
@@ -156,7 +170,7 @@ def main():
             # ResNet-50 once in three runs at 10.34 ms vs 10.06 eager, profiles/r2_bench_s19.jsonl)
             t_eager, t_graph = float("inf"), float("inf")
             for _ in range(3):
-                t_eager = min(t_eager, _time(step))
+                t_eager = min(t_eager, _time(eager))
                 t_graph = min(t_graph, _time(sg.replay))
             if world > 1:
                 # every rank takes the same decision (the slowest rank's timings)
@@ -165,7 +179,7 @@ def main():
                 dist.all_reduce(tt, op=dist.ReduceOp.MAX)
                 t_eager, t_graph = tt.tolist()
             if t_eager < t_graph:
-                run, use_graph = step, 0
+                run, use_graph = eager, 0
     for _ in range(args.warmup):
         run()
     torch.cuda.synchronize()

@@ -538,12 +538,21 @@ class HipBackend(_Common):
         real launch that follows)."""
         st = self.stream()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        best, best_t = (0, 2, False, 0), float("inf")
         cands = tuple(int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6,7,8").split(","))
         seen = set()
         modes = (False, True) if self.wgrad_atomic_ok else (False,)
+
+        def time_one(a, ns, n):
+            ev0.record()
+            for _ in range(n):
+                self._wgrad_full(a, ns, out, st)
+            ev1.record()
+            ev1.synchronize()
+            return ev0.elapsed_time(ev1) / n
+
+        first = []  # (ms, (target, pipeline, atomic, min steps), args)
         for tgt, atomic, ms_min in [(t, m, k) for t in self.WGRAD_TARGETS for m in modes
-                                for k in self.WGRAD_MIN_STEPS_CANDS]:
+                                    for k in self.WGRAD_MIN_STEPS_CANDS]:
             a = args_for(tgt, atomic, ms_min)
             if (a.splits, a.atomic_out) in seen:
                 continue
@@ -553,14 +562,18 @@ class HipBackend(_Common):
                     continue  # pipeline not available for this launch (e.g. BN-backward dY: LDS-DMA only)
                 for _ in range(2):
                     self._wgrad_full(a, ns, out, st)
-                ev0.record()
-                for _ in range(iters):
-                    self._wgrad_full(a, ns, out, st)
-                ev1.record()
-                ev1.synchronize()
-                t_ms = ev0.elapsed_time(ev1) / iters
-                if t_ms < best_t:
-                    best, best_t = (tgt, ns, bool(a.atomic_out), ms_min), t_ms
+                first.append((time_one(a, ns, iters), (tgt, ns, bool(a.atomic_out), ms_min), a))
+        if not first:
+            return (0, 2, False, 0)
+        # pass 2 (as the forward tuner): the 4 fastest re-timed twice, interleaved, each keeping its
+        # best -- single 5-launch timings of ~10-us CIFAR kernels picked outliers (run-to-run step
+        # spread 1.77-1.95 ms at batch 32)
+        first.sort(key=lambda r: r[0])
+        top = [[ms, cfg, a] for ms, cfg, a in first[:4]]
+        for _ in range(2 if len(top) > 1 else 0):
+            for r in top:
+                r[0] = min(r[0], time_one(r[2], r[1][1], 2 * iters))
+        best_t, best, _ = min(top, key=lambda r: r[0])
         if best[2]:
             self.wgrad_atomic_used = True  # the executor now zeroes the gradients every step
         self.tune_log.append((("wgrad",) + key, best, round(best_t * 1e3, 1)))

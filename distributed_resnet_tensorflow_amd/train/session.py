@@ -94,9 +94,12 @@ class TrainingSession:
         self.use_graph = use_graph and self.device.type == "cuda" and self.be.name == "hip" and (
             not dp or (dp_ok and self.engine.p2p is not None) or
             (dp_ok and os.environ.get("DRN_DP_GRAPH") == "1"))
-        if dp and not self.use_graph and self.device.type == "cuda":
+        if not self.use_graph and self.device.type == "cuda" and self.be.name == "hip":
+            # eager step (data parallel or not): the critical path on its own high-priority HW
+            # queue, ahead of the weight-gradient side stream (ResNet-50 bs128 on one GPU: 9.93 vs
+            # 10.17 ms per step, profiles/r3_side_stream_ab.txt)
             from ..parallel.engine import use_priority_main_stream
-            use_priority_main_stream()  # eager DP step: critical path on its own HW queue
+            use_priority_main_stream()
         self._graph: Optional[StepGraph] = None
         self._metrics_cache = None
         self.cur_lr = float("nan")
