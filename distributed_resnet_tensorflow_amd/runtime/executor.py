@@ -179,6 +179,10 @@ class Executor:
         # weight gradients on a second HIP stream (DRN_WGRAD_STREAM=1): every wgrad (+ its split-K
         # reduction) only feeds the optimizer, so it runs concurrently with the data-gradient /
         # BN-backward chain of the critical path; events guard the gradient buffers it reads
+        # the projection shortcut's forward conv on the side stream too (DRN_FWD_PROJ_SIDE=1): it
+        # only feeds the residual of the block's last conv, so it can run beside the main path's
+        # middle conv (the side stream is idle during the forward pass)
+        self.fwd_proj_side = os.environ.get("DRN_FWD_PROJ_SIDE", "0") == "1"
         self.side = None
         if self.is_hip and os.environ.get("DRN_WGRAD_STREAM", "1") == "1":
             cus = int(os.environ.get("DRN_SIDE_CUS", "0"))
@@ -647,19 +651,34 @@ class Executor:
         be = self.be
         bn = bp.bn
         self._bn_fwd(bn[0], train)
-        if bp.proj is not None:
+        proj_ev = None
+        side_proj = bp.proj is not None and self.side is not None and self.fwd_proj_side
+        if bp.proj is not None and not side_proj:
             xin, pro, fin = self._cin(bn[0])
             be.conv_fwd(xin, bp.proj.w, bp.sc, bp.proj.geom, in_bn=pro, in_fin=fin)
         for i, op in enumerate(bp.convs):
             last = i == len(bp.convs) - 1
             xin, pro, fin = self._cin(bn[i])
             if last:
+                if proj_ev is not None:
+                    torch.cuda.current_stream(self.device).wait_event(proj_ev)
                 res = bp.sc if bp.proj is not None else bp.x
                 be.conv_fwd(xin, op.w, bp.out, op.geom, in_bn=pro, residual=res, in_fin=fin,
                             stats=bp.out_stats if train else None, bn_fin=self._fin_fwd(bp.out_stats, train))
             else:
                 be.conv_fwd(xin, op.w, bp.hs[i], op.geom, in_bn=pro, in_fin=fin,
                             stats=bn[i + 1].stats if train else None, bn_fin=self._fin_fwd(bn[i + 1].stats, train))
+                if i == 0 and side_proj:
+                    # fork the shortcut conv behind conv1 (which finalized and published bn1: the
+                    # shortcut reads the published scale/shift) so it runs beside conv2; joined
+                    # before the last conv, whose epilogue adds it
+                    main = torch.cuda.current_stream(self.device)
+                    self.side.wait_stream(main)
+                    pxin, ppro, pfin = self._cin(bn[0])
+                    with torch.cuda.stream(self.side):
+                        be.conv_fwd(pxin, bp.proj.w, bp.sc, bp.proj.geom, in_bn=ppro, in_fin=pfin)
+                    proj_ev = torch.cuda.Event()
+                    proj_ev.record(self.side)
                 self._bn_fwd(bn[i + 1], train)
 
     # ------------------------------------------------------------------------------------------
