@@ -493,17 +493,18 @@ class Executor:
         # critical path on the high-priority stream the side stream runs further behind: ResNet-50
         # bs128, one box, 3 rounds: 6 buffers 10.13-10.22 ms, 16: 10.07-10.13, 24: 10.01-10.05
         # (profiles/r3s2_gradbufs.txt). Default 32 (~6.5 GB at ResNet-50 bs128), at most ~8 % of
-        # the device memory.
+        # the device memory, for ImageNet-sized activations; small ones (CIFAR: latency-bound
+        # kernels on L2-resident tensors, 2.06-2.28 ms with 32 buffers vs 1.8-2.1 ms) keep 6.
         nbuf_env = os.environ.get("DRN_GRAD_BUFS")
+        buf_bytes = max_act * torch.finfo(self.be.act_dtype).bits // 8
         if nbuf_env is not None:
             nbuf = max(3, int(nbuf_env))
-        elif self.side is not None:
-            buf_bytes = max_act * torch.finfo(self.be.act_dtype).bits // 8
+        elif self.side is not None and buf_bytes >= (64 << 20):
             cap = int(0.08 * torch.cuda.get_device_properties(self.device).total_memory) // max(1, buf_bytes) \
                 if self.device.type == "cuda" else 32
             nbuf = max(6, min(32, cap))
         else:
-            nbuf = 3
+            nbuf = 6 if self.side is not None else 3
         self.g_bufs = [self._act(max_act) for _ in range(nbuf)]
         self.g_a, self.g_b, self.g_c = self.g_bufs[:3]
         self._lru: List[int] = []
