@@ -495,11 +495,17 @@ class Executor:
         # (profiles/r3s2_gradbufs.txt). Default 32 (~6.5 GB at ResNet-50 bs128), at most ~8 % of
         # the device memory, for ImageNet-sized activations; small ones (CIFAR: latency-bound
         # kernels on L2-resident tensors, 2.06-2.28 ms with 32 buffers vs 1.8-2.1 ms) keep 6.
+        # Multi-rank data parallelism keeps 6: the bucket all-reduces are issued from the side
+        # stream once it has caught up (_report), so a side stream running further behind would
+        # start them later and expose more communication after the backward pass (unmeasured at
+        # N > 1: no multi-GPU box here).
         nbuf_env = os.environ.get("DRN_GRAD_BUFS")
         buf_bytes = max_act * torch.finfo(self.be.act_dtype).bits // 8
+        import torch.distributed as _dist
+        multi_rank = _dist.is_available() and _dist.is_initialized() and _dist.get_world_size() > 1
         if nbuf_env is not None:
             nbuf = max(3, int(nbuf_env))
-        elif self.side is not None and buf_bytes >= (64 << 20):
+        elif self.side is not None and buf_bytes >= (64 << 20) and not multi_rank:
             cap = int(0.08 * torch.cuda.get_device_properties(self.device).total_memory) // max(1, buf_bytes) \
                 if self.device.type == "cuda" else 32
             nbuf = max(6, min(32, cap))
