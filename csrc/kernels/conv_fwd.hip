@@ -1691,10 +1691,6 @@ DRN_API int drn_conv_fwd_tiles_p(int M, int K) {
 
 DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s);
 
-// multi-tile LDS-DMA family (conv_mt.hip): config ids DRN_GLDS_NCFG .. + drn_conv_mt_num_cfgs()
-DRN_API int drn_conv_mt(int cfg, DrnConvFwdArgs* a, const void* zero, hipStream_t s);
-DRN_API int drn_conv_mt_num_cfgs();
-DRN_API int drn_conv_mt_ok(const DrnConvFwdArgs* a);
 #define DRN_GLDS_NCFG 38
 
 // Whether the LDS-DMA kernel family supports this convolution.
@@ -1725,7 +1721,7 @@ DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
       (a->cfg < 0 || a->cfg >= DRN_GLDS_NCFG || !drn_conv_glds_ok(a) || zero == nullptr))
     return (int)hipErrorInvalidValue;  // split-K: explicit split-capable LDS-DMA configurations only
   if (a->cfg >= DRN_NK_CFG0 && a->cfg < DRN_NK_CFG0 + DRN_NK_NCFG) return drn::launch_conv_nk(a->cfg - DRN_NK_CFG0, a, s);
-  if (a->cfg >= DRN_GLDS_NCFG && a->cfg != 100) return drn_conv_mt(a->cfg - DRN_GLDS_NCFG, a, zero, s);
+  if (a->cfg >= DRN_GLDS_NCFG && a->cfg != 100) return (int)hipErrorInvalidValue;
   if (a->bnb_x != nullptr && (!drn_conv_glds_ok(a) || zero == nullptr || a->cfg == 100))
     return (int)hipErrorInvalidValue;  // the BN-backward input transform exists on the LDS-DMA path only
   if (drn_conv_glds_ok(a) && zero != nullptr && a->cfg != 100)
@@ -1763,7 +1759,7 @@ DRN_API int drn_conv_sk_slots_cfg(const DrnConvFwdArgs* a, int cfg, int G) {
 // narrow-output (K = 16 / 32) register-operand kernels: configuration ids DRN_NK_CFG0 + i
 DRN_API int drn_conv_nk_num_cfgs() { return DRN_NK_NCFG; }
 DRN_API int drn_conv_nk_cfg0() { return DRN_NK_CFG0; }
-DRN_API int drn_conv_glds_num_cfgs() { return DRN_GLDS_NCFG + drn_conv_mt_num_cfgs(); }
+DRN_API int drn_conv_glds_num_cfgs() { return DRN_GLDS_NCFG; }
 DRN_API int drn_conv_glds_default_cfg(const DrnConvFwdArgs* a) { return drn::glds_default_cfg(a); }
 
 DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s) {

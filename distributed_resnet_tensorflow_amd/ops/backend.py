@@ -381,7 +381,7 @@ class HipBackend(_Common):
         cands = os.environ.get("DRN_CONV_CANDS")
         if cands:
             cands = [int(c) for c in cands.split(",")]
-        else:  # register-staged, LDS-DMA + multi-tile, narrow-output (K = 16 / 32) configurations
+        else:  # register-staged, LDS-DMA, narrow-output (K = 16 / 32) configurations
             nk0 = self.L.drn_conv_nk_cfg0()
             cands = [100] + list(range(self.L.drn_conv_glds_num_cfgs())) + \
                 [nk0 + i for i in range(self.L.drn_conv_nk_num_cfgs())] * (a.K in (16, 32))

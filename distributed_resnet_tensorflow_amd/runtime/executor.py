@@ -30,7 +30,7 @@ from typing import Callable, List, Optional
 import torch
 
 from ..models.spec import Block, BN, Conv, NetSpec
-from ..ops.backend import BnCfin, BnFin, ConvGeom, OutMap, dgrad_geom, tflip_desc, tflip_table
+from ..ops.backend import BnCfin, ConvGeom, OutMap, dgrad_geom, tflip_desc, tflip_table
 from .params import ParamStore
 
 BN_DECAY = 0.997     # reference resnet_model_official.py:37
@@ -57,10 +57,6 @@ class BNState:
     act: Optional[torch.Tensor] = None     # materialised relu(bn(src)) (materialize_bn mode)
     bacc: Optional[torch.Tensor] = None    # backward sums [R][2][C] (sum g, sum g*xhat)
     bG: int = 1                            # replicas of bacc
-    fin_f: Optional[torch.Tensor] = None   # int32 arrival counters of the fused forward finalize
-    fin_b: Optional[torch.Tensor] = None   # ... and of the fused backward finalize
-    fin_done: bool = False                 # this step's forward finalize ran inside the producer conv
-    bfin_done: bool = False                # this step's backward finalize ran inside the dgrad
     cfin_pub: bool = False                 # consumer-side finalize: the next consumer publishes
 
     @property
@@ -103,28 +99,6 @@ class BlockPlan:
     grad_lo: int                    # lowest flat grad offset written by this block
 
 
-def _cu_masked_stream(device, n_cus: int):
-    """A HIP stream whose kernels may only occupy n_cus of the GPU's CUs (hipExtStreamCreateWithCUMask,
-    CUs taken evenly over the whole index range so every XCD contributes): the weight-gradient side
-    stream then leaves the rest of the chip free for the critical-path data gradients instead of
-    holding every CU slot with long-lived blocks (DRN_SIDE_CUS; eager steps -- a captured graph does
-    not keep a stream's CU mask)."""
-    import ctypes
-    hip = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
-    total = torch.cuda.get_device_properties(device).multi_processor_count
-    n_cus = max(1, min(n_cus, total))
-    words = (ctypes.c_uint32 * ((total + 31) // 32))()
-    for j in range(n_cus):
-        cu = (j * total) // n_cus
-        words[cu // 32] |= 1 << (cu % 32)
-    st = ctypes.c_void_p()
-    with torch.cuda.device(device):
-        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(len(words)), words)
-    if rc != 0:
-        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
-    return torch.cuda.ExternalStream(st.value, device=device)
-
-
 class Executor:
     def __init__(self, spec: NetSpec, batch: int, backend, device, seed: int = 0,
                  weight_decay: float = 2e-4, momentum: float = 0.9, params: ParamStore | None = None,
@@ -155,22 +129,15 @@ class Executor:
             self.fuse_bn_bwd = False
             if hasattr(backend, "autotune"):
                 backend.autotune = False  # timing-dependent tile choices change per-tile partial sums
-        # BN finalize (forward and backward) folded into the streaming apply kernels
-        # (measured: a win in the backward apply, a loss in the forward apply, whose per-thread
-        # finalize prologue costs more than the separate C-thread finalize launch)
-        self.fuse_finalize = os.environ.get("DRN_FUSE_BN_FINALIZE", "0") == "1"
-        # BN finalize inside the conv producing the statistics (last-arriving workgroup per
-        # channel column, DRN_FUSE_BN_FIN=1): removes ~100 small finalize launches per ImageNet
-        # step, but every workgroup must then wait for its atomics and a counter round trip
-        # before it retires -- measured 12.85 ms vs 11.78 ms per ResNet-50 step, so off
-        self.fuse_fin = os.environ.get("DRN_FUSE_BN_FIN", "0") == "1" and not self.deterministic
-        self.fuse_finalize_fwd = os.environ.get("DRN_FUSE_BN_FINALIZE_FWD", "0") == "1"
+        # (Producer-side finalize variants -- the last-arriving conv workgroup per channel column,
+        # or the streaming apply kernels finalizing G == 1 statistics -- measured slower than the
+        # consumer-side finalize below (ResNet-50: 12.85 vs 11.78 ms) and were removed.)
         # Consumer-side BN finalize (DRN_CFIN, default on for HIP): no finalize launches at all --
         # the kernels CONSUMING a BatchNorm (the fused-prologue 1x1 convs, the materialising
         # apply, the backward apply) derive its parameters from the statistics replicas in their
         # own prologue and the first of them publishes them (ops/backend.py BnCfin). Removes ~98
         # dependent ~6 us launches per ResNet-50 step from the critical path.
-        self.cfin = not self.deterministic and not self.fuse_fin and os.environ.get("DRN_CFIN", "1") == "1"
+        self.cfin = not self.deterministic and os.environ.get("DRN_CFIN", "1") == "1"
         # single-phase strided data gradients zero the other phases in their own epilogue
         self.out_fill = os.environ.get("DRN_OUT_FILL", "1") == "1"
         self.device = torch.device(device)
@@ -178,15 +145,14 @@ class Executor:
         self.is_hip = backend.name == "hip"
         # weight gradients on a second HIP stream (DRN_WGRAD_STREAM=1): every wgrad (+ its split-K
         # reduction) only feeds the optimizer, so it runs concurrently with the data-gradient /
-        # BN-backward chain of the critical path; events guard the gradient buffers it reads
-        # the projection shortcut's forward conv on the side stream too (DRN_FWD_PROJ_SIDE=1): it
-        # only feeds the residual of the block's last conv, so it can run beside the main path's
-        # middle conv (the side stream is idle during the forward pass)
-        self.fwd_proj_side = os.environ.get("DRN_FWD_PROJ_SIDE", "0") == "1"
+        # BN-backward chain of the critical path; events guard the gradient buffers it reads.
+        # Only weight gradients (conv_wgrad, its own workspace) run there: the split-K conv
+        # workspace and tickets of the backend are used by main-stream launches alone.
+        # (Forking the projection-shortcut forward conv onto this stream measured neutral, and a
+        # CU-masked side stream +0-0.4 %; both were removed.)
         self.side = None
         if self.is_hip and os.environ.get("DRN_WGRAD_STREAM", "1") == "1":
-            cus = int(os.environ.get("DRN_SIDE_CUS", "0"))
-            self.side = _cu_masked_stream(self.device, cus) if cus > 0 else torch.cuda.Stream(self.device)
+            self.side = torch.cuda.Stream(self.device)
         self._pending = {}
         # BN-apply+ReLU either fused into every consuming conv's load prologue (recomputed by the
         # forward conv, the projection conv and both weight-gradient convs; the LDS-DMA kernels
@@ -321,23 +287,6 @@ class Executor:
         """Every BatchNorm of the network in TF creation order."""
         return [b for bp in self.blocks for b in bp.bn] + [self.final_bn]
 
-    def _fin_counters(self) -> torch.Tensor:
-        t = self._fin_words[self._fin_off:self._fin_off + 64]
-        self._fin_off += 64
-        assert t.numel() == 64, "fused-finalize counter arena exhausted"
-        return t
-
-    def _fin_fwd(self, stats, train: bool):
-        """The BnFin that lets the conv producing `stats` finalize the BN consuming them."""
-        if not (train and self.fuse_fin) or stats is None:
-            return None
-        b = self._bn_by_stats.get(stats.data_ptr())
-        if b is None:
-            return None
-        b.fin_done = True
-        return BnFin(b.fin_f, b.rows, b.gamma, beta=b.beta, run_mean=b.run_mean, run_var=b.run_var, scale=b.scale,
-                     shift=b.shift, mean=b.mean, invstd=b.invstd, momentum=BN_DECAY, eps=BN_EPSILON)
-
     def _alloc(self):
         sp, N = self.spec, self.N
         be = self.be
@@ -349,13 +298,8 @@ class Executor:
             arena = 64 + sum(2 * ((2 * c * self._det_replicas(m, c) + 15) // 16 * 16) for m, c in self._bn_shapes())
         else:
             arena = sum(2 * ((2 * c * self._reps(c) + 15) // 16 * 16) for c in all_c) + 64
-        # + the arrival counters of the fused finalizes (64 per BN and direction), cleared with
-        # the statistics by the same per-step fill
-        n_bn = len(all_c) + 1
         self._arena_cap = arena
-        self.stats_arena = self._f32(arena + 2 * 64 * n_bn)
-        self._fin_words = self.stats_arena[arena:].view(torch.int32)
-        self._fin_off = 0
+        self.stats_arena = self._f32(arena)
         self._arena_off = 0
         wt_descs, wt_off = [], 0
         self.stem_op, wt_off = self._conv_op(sp.stem, wt_descs, wt_off)
@@ -471,8 +415,6 @@ class Executor:
                     b.act = self._act(*b.src.shape)
         for b in [b for bp in self.blocks for b in bp.bn] + [self.final_bn]:
             b.bacc, b.bG = self._stats_for(b.rows, b.bn.c)
-            b.fin_f, b.fin_b = self._fin_counters(), self._fin_counters()
-        self._bn_by_stats = {b.stats.data_ptr(): b for b in [b for bp in self.blocks for b in bp.bn] + [self.final_bn]}
         self.last_out = x
         C, ncls = sp.final_c, sp.num_classes
         self.pooled = self._f32(N, C)
@@ -581,15 +523,6 @@ class Executor:
             else:
                 b.cfin_pub = True
             return
-        if train and b.fin_done:  # finalized by the producing conv
-            b.fin_done = False
-            if b.act is not None:
-                self.be.bn_apply(b.src, b.act, b.scale, b.shift, relu=True)
-            return
-        if train and b.act is not None and self.fuse_finalize_fwd and b.G == 1:
-            self.be.bn_apply_stats(b.src, b.act, b.stats, b.rows, b.gamma, b.beta, b.run_mean, b.run_var, b.scale,
-                                   b.shift, b.mean, b.invstd, BN_DECAY, BN_EPSILON, relu=True)
-            return
         if train:
             self.be.bn_finalize(b.stats, b.G, b.rows, b.gamma, b.beta, b.run_mean, b.run_var, b.scale, b.shift,
                                 b.mean, b.invstd, BN_DECAY, BN_EPSILON, update_running=True)
@@ -614,10 +547,9 @@ class Executor:
         if self.stem_pack:
             be.stem_pack_input(self.images, self.stem_xp)
             be.conv_fwd(self.stem_xp, self.stem_w4, self.stem_out, self.stem_geom4,
-                        stats=self.stem_stats if train else None, bn_fin=self._fin_fwd(self.stem_stats, train))
+                        stats=self.stem_stats if train else None)
         else:
-            be.conv_fwd(self.images, st.w, self.stem_out, st.geom, stats=self.stem_stats if train else None,
-                        bn_fin=self._fin_fwd(self.stem_stats, train))
+            be.conv_fwd(self.images, st.w, self.stem_out, st.geom, stats=self.stem_stats if train else None)
         if sp.maxpool:
             ph = sp.pool_hw
             pad = max((ph - 1) * 2 + 3 - sp.stem_hw, 0) // 2
@@ -658,34 +590,19 @@ class Executor:
         be = self.be
         bn = bp.bn
         self._bn_fwd(bn[0], train)
-        proj_ev = None
-        side_proj = bp.proj is not None and self.side is not None and self.fwd_proj_side
-        if bp.proj is not None and not side_proj:
+        if bp.proj is not None:
             xin, pro, fin = self._cin(bn[0])
             be.conv_fwd(xin, bp.proj.w, bp.sc, bp.proj.geom, in_bn=pro, in_fin=fin)
         for i, op in enumerate(bp.convs):
             last = i == len(bp.convs) - 1
             xin, pro, fin = self._cin(bn[i])
             if last:
-                if proj_ev is not None:
-                    torch.cuda.current_stream(self.device).wait_event(proj_ev)
                 res = bp.sc if bp.proj is not None else bp.x
                 be.conv_fwd(xin, op.w, bp.out, op.geom, in_bn=pro, residual=res, in_fin=fin,
-                            stats=bp.out_stats if train else None, bn_fin=self._fin_fwd(bp.out_stats, train))
+                            stats=bp.out_stats if train else None)
             else:
                 be.conv_fwd(xin, op.w, bp.hs[i], op.geom, in_bn=pro, in_fin=fin,
-                            stats=bn[i + 1].stats if train else None, bn_fin=self._fin_fwd(bn[i + 1].stats, train))
-                if i == 0 and side_proj:
-                    # fork the shortcut conv behind conv1 (which finalized and published bn1: the
-                    # shortcut reads the published scale/shift) so it runs beside conv2; joined
-                    # before the last conv, whose epilogue adds it
-                    main = torch.cuda.current_stream(self.device)
-                    self.side.wait_stream(main)
-                    pxin, ppro, pfin = self._cin(bn[0])
-                    with torch.cuda.stream(self.side):
-                        be.conv_fwd(pxin, bp.proj.w, bp.sc, bp.proj.geom, in_bn=ppro, in_fin=pfin)
-                    proj_ev = torch.cuda.Event()
-                    proj_ev.record(self.side)
+                            stats=bn[i + 1].stats if train else None)
                 self._bn_fwd(bn[i + 1], train)
 
     # ------------------------------------------------------------------------------------------
@@ -710,14 +627,6 @@ class Executor:
             be.bn_bwd_apply_fin(dy, dpool, pool_hw, x, b.scale, b.shift, fin, add, dx, relu=not reduced)
             return
         coef = self.bn_coef[:3 * b.bn.c]
-        if b.bfin_done:  # finalized by the producing data-gradient conv
-            b.bfin_done = False
-            be.bn_bwd_apply(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, coef, add, dx, relu=not reduced)
-            return
-        if self.fuse_finalize and G == 1:
-            be.bn_bwd_apply_stats(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, part, M, b.gamma,
-                                  b.dgamma, b.dbeta, add, dx, coef=coef, relu=not reduced)
-            return
         be.bn_finalize_bwd(part, G, M, b.gamma, b.invstd, b.dgamma, b.dbeta, coef)
         be.bn_bwd_apply(dy, dpool, pool_hw, x, b.scale, b.shift, b.mean, b.invstd, coef, add, dx,
                         relu=not reduced)
@@ -845,19 +754,13 @@ class Executor:
             and op.dg[0].out_map is not None and bn is None
         if not accumulate and not op.full_cover and not fill:
             self.be.zero_(dx)
-        fuse = fin = None
+        fuse = None
         if bn is not None:
             assert op.full_cover
             fuse = (bn_x, bn.scale, bn.shift, bn.mean, bn.invstd)
-            if self.fuse_fin:  # the last phase launch finalizes the BN backward too
-                C = bn.bn.c
-                fin = BnFin(bn.fin_b, bn.rows, bn.gamma, dgamma=bn.dgamma, dbeta=bn.dbeta, coef=self.bn_coef[:3 * C])
-                bn.bfin_done = True
-        last = len(op.dg) - 1
-        for k, ph in enumerate(op.dg):
+        for ph in op.dg:
             self.be.conv_fwd(dy, ph.wt, dx, ph.geom, residual=dx if accumulate else None, out_map=ph.out_map,
-                             stats=bn.bacc if fuse is not None else None, bn_bwd=fuse,
-                             bn_fin=fin if k == last else None, out_fill=fill, bnb=bnb)
+                             stats=bn.bacc if fuse is not None else None, bn_bwd=fuse, out_fill=fill, bnb=bnb)
 
     def _block_bwd(self, bp: BlockPlan, bufs, cur: int) -> int:
         """Back-propagates one block; bufs[cur] holds d(block output). Returns the index of the

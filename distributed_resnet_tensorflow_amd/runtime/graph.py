@@ -48,8 +48,9 @@ class SegmentedStepGraph:
     """
 
     def __init__(self, ex, engine, grad_scale: float, warmup: int = 1):
-        if engine.p2p is not None or engine.mode != "sync":
-            raise ValueError("segmented graphs are for the synchronous RCCL/gloo engine")
+        if engine.p2p is not None or engine.mode != "sync" or engine.zero1:
+            # (ZeRO-1 updates per-rank shards and all-gathers the weights: not one captured SGD)
+            raise ValueError("segmented graphs are for the synchronous, unsharded RCCL/gloo engine")
         self.ex, self.eng, self.grad_scale = ex, engine, grad_scale
         # a capture may end only when every forked stream has joined: the side-stream weight
         # gradients (reported one block late) would straddle the cut points, so this step keeps
@@ -72,10 +73,15 @@ class SegmentedStepGraph:
                 ex.backward()
             finally:
                 ex.grad_ready = None
-            ex.apply_gradients(grad_scale=grad_scale, grad=ex.P.grad)
+            # the SGD segment reads the buffer finish() returns: with the bf16 wire that is the
+            # reduced bf16 shadow, never the rank-local fp32 gradient
+            ex.apply_gradients(grad_scale=grad_scale, grad=self._reduced_grad())
             self._close(None)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+
+    def _reduced_grad(self):
+        return self.eng.wire_buf if self.eng.wire_buf is not None else self.ex.P.grad
 
     def _eager(self):
         ex, eng = self.ex, self.eng
@@ -105,5 +111,6 @@ class SegmentedStepGraph:
         for g, lo in self.segments[:-1]:
             g.replay()
             eng._on_ready(lo)
-        eng.finish()
+        g = eng.finish()
+        assert g is self._reduced_grad(), "the captured SGD segment reads a different gradient buffer"
         self.segments[-1][0].replay()

@@ -29,16 +29,16 @@ log = logging.getLogger("drn")
 
 def make_backend(device: str, precision: str = "bf16"):
     """--precision: bf16 = the gfx950 HIP kernel library (bf16 activations / weights, fp32
-    accumulation, fp32 master weights, momentum and BN statistics); fp32 = the fp32 PyTorch
-    reference backend on the same device (a numerics-debugging path, not a performance one).
-    CPU runs always use the fp32 reference backend."""
+    accumulation, fp32 master weights, momentum and BN statistics) -- the only GPU path: the
+    product never routes a convolution to a vendor library (MIOpen). fp32 is the CPU reference
+    backend (the fp32 PyTorch oracle ops); asking for it on a GPU is an error. CPU runs always
+    use the fp32 reference backend."""
     if precision not in ("bf16", "fp32"):
         raise ValueError(f"--precision must be bf16 or fp32, got {precision!r}")
     if str(device).startswith("cuda"):
         if precision == "fp32":
-            log.warning("--precision=fp32: fp32 PyTorch reference ops on %s (debug path; the HIP kernels are bf16)",
-                        device)
-            return RefBackend(device)
+            raise ValueError("--precision=fp32 is the CPU reference path; the GPU path is the bf16 HIP kernel "
+                             "library (fp32 accumulation, fp32 master weights)")
         return HipBackend(device)
     return RefBackend("cpu")
 

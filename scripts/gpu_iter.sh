@@ -3,7 +3,7 @@
 # bench + kernel-trace profile, optional extra probes. Stops at the first failure.
 #   TESTS="tests/test_x.py ..." K="pytest -k expression" SWEEP=1 BENCH=1 PROBE="cmd" scripts/gpu_iter.sh <outdir>
 OUT=${1:-gpurun_out/iter}
-TESTS=${TESTS:-"tests/test_ops_gpu.py tests/test_conv_mt_gpu.py"}
+TESTS=${TESTS:-"tests/test_ops_gpu.py"}
 K=${K:-""}
 export PYTHONPATH=$(pwd)
 mkdir -p "$OUT"

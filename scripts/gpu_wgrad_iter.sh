@@ -7,7 +7,7 @@ OUT=${1:-gpurun_out/witer}
 export PYTHONPATH=$(pwd)
 mkdir -p "$OUT"
 if [ "${TESTS:-}" != "none" ]; then
-  timeout -k 10 900 python -u -m pytest ${TESTS:-tests/test_ops_gpu.py tests/test_conv_mt_gpu.py tests/test_executor_gpu.py} \
+  timeout -k 10 900 python -u -m pytest ${TESTS:-tests/test_ops_gpu.py tests/test_executor_gpu.py} \
     -m gpu -x -q --timeout 170 --timeout-method thread > "$OUT/tests.log" 2>&1
   rc=$?; tail -2 "$OUT/tests.log"
   if [ $rc -ne 0 ]; then grep -E "Error|assert|FAILED" "$OUT/tests.log" | head -20; exit $rc; fi

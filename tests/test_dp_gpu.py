@@ -109,9 +109,9 @@ def test_dp_engine_gpu_two_ranks_one_device(allreduce):
         assert same
 
 
-def _seg_worker(rank, world, port, q):
+def _seg_worker(rank, world, port, q, wire="fp32"):
     try:
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DRN_ALLREDUCE_WIRE=wire)
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2
@@ -139,7 +139,13 @@ def _seg_worker(rank, world, port, q):
         sg.replay()
         torch.cuda.synchronize()
         err = ((ea.P.master - eb.P.master).norm() / ea.P.master.norm()).item()
-        q.put((rank, err, len(sg.segments) > 3 and bool(torch.isfinite(eb.P.master).all())))
+        # every rank must hold the same weights: a segment that updated from the rank-local
+        # (unreduced) gradient would make the two ranks diverge
+        out = eb.P.master.double().sum().reshape(1).cpu()
+        gathered = [torch.zeros_like(out) for _ in range(world)]
+        dist.all_gather(gathered, out)
+        same = all(torch.equal(gathered[0], t) for t in gathered)
+        q.put((rank, err, len(sg.segments) > 3 and bool(torch.isfinite(eb.P.master).all()) and same))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover
@@ -147,13 +153,15 @@ def _seg_worker(rank, world, port, q):
         q.put((rank, repr(e) + traceback.format_exc(), False))
 
 
-def test_segmented_graph_dp_step_matches_eager():
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_segmented_graph_dp_step_matches_eager(wire):
     """Per-segment HIP graphs with host-issued all-reduces between them (the N>1 bench / training
-    path) reproduce the eager data-parallel step."""
+    path) reproduce the eager data-parallel step, with fp32 or bf16 gradients on the wire (the
+    captured SGD segment must read the reduced bf16 buffer, not the rank-local gradient)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_seg_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_seg_worker, args=(r, 2, port, q, wire)) for r in range(2)]
     for p in ps:
         p.start()
     res = [q.get(timeout=300) for _ in ps]
