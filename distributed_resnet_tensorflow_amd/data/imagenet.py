@@ -243,6 +243,33 @@ def _shm_cleanup(pid: int) -> None:
             pass
 
 
+def _shm_cleanup_stale() -> int:
+    """Unlink decode segments whose loader process no longer exists (a loader that died by
+    SIGKILL, OOM or os._exit never ran its atexit cleanup). Segment names carry the loader's pid
+    (`drn_dec_<loader pid>_<worker pid>_<seq>`). Returns the number of segments removed."""
+    n = 0
+    for f in glob.glob(f"/dev/shm/{_SHM_PREFIX}*"):
+        try:
+            pid = int(os.path.basename(f)[len(_SHM_PREFIX):].split("_", 1)[0])
+        except ValueError:
+            continue
+        if pid == os.getpid():
+            continue
+        try:
+            os.kill(pid, 0)
+            continue                   # the loader is alive (this user's or another's): keep
+        except ProcessLookupError:
+            pass
+        except PermissionError:
+            continue                   # alive, owned by another user
+        try:
+            os.unlink(f)
+            n += 1
+        except OSError:
+            pass
+    return n
+
+
 def _decode_chunk_in_worker(items):
     """Several records per task (fewer pool round trips): [(path, r)] -> [((shm, shape), label)]."""
     return [_decode_in_worker(p, r) for p, r in items]
@@ -308,6 +335,7 @@ class ImagenetLoader:
             # spawn: never fork a process that holds a GPU context
             self.pool = ProcessPoolExecutor(max_workers=max(1, num_threads), mp_context=mp.get_context("spawn"))
             atexit.register(_shm_cleanup, os.getpid())
+            _shm_cleanup_stale()       # leftovers of loaders that died without their atexit
         else:
             self.pool = ThreadPoolExecutor(max_workers=max(1, num_threads))
         self.q: "queue.Queue" = queue.Queue(maxsize=max(1, prefetch))

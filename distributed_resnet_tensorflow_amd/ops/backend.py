@@ -246,6 +246,18 @@ class HipBackend(_Common):
         forced = os.environ.get("DRN_WGRAD_NS")
         self.forced_wgrad_ns = int(forced) if forced not in (None, "") else None
         self.tune_log: list = []
+        self._db = None   # persistent kernel-selection database (ops/tunedb.py), loaded on first use
+        self.db_hits = 0
+
+    def tune_db(self):
+        if self._db is None:
+            from .tunedb import TuneDB, section_for
+            self._db = TuneDB(section_for(self.device, self.L))
+        return self._db
+
+    def save_tune_db(self) -> bool:
+        """Persist the configurations timed by this process (no-op when nothing new was tuned)."""
+        return self._db is not None and self._db.save()
 
     def stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -348,7 +360,13 @@ class HipBackend(_Common):
         if a.cfg == -1 and self.autotune and self.forced_cfg is None:
             key = self.conv_key(a)
             if key not in self.conv_cfg and not torch.cuda.is_current_stream_capturing():
-                self.conv_cfg[key] = self._tune_conv(a, key)
+                hit = self.tune_db().get_conv(key)
+                if hit is not None:
+                    self.db_hits += 1
+                    self.conv_cfg[key] = hit
+                else:
+                    self.conv_cfg[key] = self._tune_conv(a, key)
+                    self.tune_db().put_conv(key, self.conv_cfg[key])
             cfg, ks = self.conv_cfg.get(key, (-1, 1))
             a.cfg = cfg
             self._set_ksplit(a, ks)
@@ -589,7 +607,15 @@ class HipBackend(_Common):
             return
         key = self.wgrad_key(a)
         if key not in self.wgrad_ns and self.autotune and not torch.cuda.is_current_stream_capturing():
-            self.wgrad_ns[key] = self._tune_wgrad(args_for, out, key)
+            hit = self.tune_db().get_wgrad(key)
+            if hit is not None and (not hit[2] or self.wgrad_atomic_ok):
+                self.db_hits += 1
+                self.wgrad_ns[key] = hit
+                if hit[2]:
+                    self.wgrad_atomic_used = True  # the executor now zeroes the gradients every step
+            else:
+                self.wgrad_ns[key] = self._tune_wgrad(args_for, out, key)
+                self.tune_db().put_wgrad(key, self.wgrad_ns[key])
             if self.wgrad_ns[key][2]:
                 self.zero_(out)  # the timing launches left partial sums in this gradient slot
         tgt, ns, atomic, ms = self.wgrad_ns.get(key, (0, 2, False, 0))

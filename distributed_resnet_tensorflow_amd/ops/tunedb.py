@@ -1,0 +1,131 @@
+"""Persistent kernel-selection database: the analog of MIOpen's find-db / perf-db.
+
+The HIP backend picks a kernel configuration per convolution geometry by timing candidates
+(ops/backend.py `_tune_conv`, `_tune_wgrad`). Timing is noisy (clock ramps, neighbours' cache
+state), so two runs of the same library could pick different tiles and differ by several percent
+(CIFAR bs32: 1.77-1.95 ms across runs). The choices are therefore persisted and reused: a
+geometry found in the database is never re-timed, so runs of one library are deterministic and
+start without the tuning pass.
+
+Entries are keyed by
+  * the device architecture (gcnArchName, e.g. ``gfx950:sramecc+:xnack-``) and CU count,
+  * the kernel library's source hash (``drn_src_hash``, ops/build.py): a rebuilt library with
+    other kernels never reuses stale choices,
+  * the geometry key the backend already uses (conv_key / wgrad_key).
+
+File: ``DRN_TUNE_DB`` (``off`` disables it), default ``ops/tune_db.json`` next to the library, so
+a database produced on an MI355X ships with the tree. Writes are read-merge-write through a
+temporary file and ``os.replace`` (several ranks of one node may write concurrently; the last
+rename wins, every version is a complete file). Sections of other library hashes are dropped
+when a section is written (they can never match again).
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+from pathlib import Path
+from typing import Optional
+
+VERSION = 1
+DEFAULT_PATH = Path(__file__).resolve().parent / "tune_db.json"
+_LOCK = threading.Lock()
+
+
+def db_path() -> Optional[Path]:
+    p = os.environ.get("DRN_TUNE_DB", "")
+    if p.lower() in ("off", "0", "none"):
+        return None
+    return Path(p) if p else DEFAULT_PATH
+
+
+def _key(t) -> str:
+    return ",".join(str(int(v)) if isinstance(v, (bool, int)) else str(v) for v in t)
+
+
+class TuneDB:
+    """One section (device + library) of the database, loaded lazily."""
+
+    def __init__(self, section: str, path: Optional[Path] = None):
+        self.section = section
+        self.path = db_path() if path is None else path
+        self.conv: dict = {}
+        self.wgrad: dict = {}
+        self.dirty = False
+        if self.path is not None and self.path.exists():
+            try:
+                data = json.loads(self.path.read_text())
+                sec = data.get("sections", {}).get(section, {}) if data.get("version") == VERSION else {}
+                self.conv = dict(sec.get("conv", {}))
+                self.wgrad = dict(sec.get("wgrad", {}))
+            except (OSError, ValueError):
+                self.conv, self.wgrad = {}, {}
+
+    # conv: (config id, split-K factor / -stream-K grid)
+    def get_conv(self, key) -> Optional[tuple]:
+        v = self.conv.get(_key(key))
+        return (int(v[0]), int(v[1])) if v is not None else None
+
+    def put_conv(self, key, val) -> None:
+        self.conv[_key(key)] = [int(val[0]), int(val[1])]
+        self.dirty = True
+
+    # wgrad: (split target, pipeline, atomic, min steps)
+    def get_wgrad(self, key) -> Optional[tuple]:
+        v = self.wgrad.get(_key(key))
+        return (int(v[0]), int(v[1]), bool(v[2]), int(v[3])) if v is not None else None
+
+    def put_wgrad(self, key, val) -> None:
+        self.wgrad[_key(key)] = [int(val[0]), int(val[1]), bool(val[2]), int(val[3])]
+        self.dirty = True
+
+    def save(self) -> bool:
+        """Merge this section into the file (entries already on disk for this section are kept
+        unless this process has its own choice for the same key). Returns True if written."""
+        if self.path is None or not self.dirty:
+            return False
+        with _LOCK:
+            data = {"version": VERSION, "sections": {}}
+            if self.path.exists():
+                try:
+                    old = json.loads(self.path.read_text())
+                    if old.get("version") == VERSION:
+                        data = old
+                except (OSError, ValueError):
+                    pass
+            arch = self.section.split("|", 1)[0]
+            # drop sections of other library builds on this device (never valid again)
+            secs = {k: v for k, v in data.get("sections", {}).items()
+                    if k == self.section or k.split("|", 1)[0] != arch}
+            sec = secs.get(self.section, {"conv": {}, "wgrad": {}})
+            sec["conv"] = {**sec.get("conv", {}), **self.conv}
+            sec["wgrad"] = {**sec.get("wgrad", {}), **self.wgrad}
+            secs[self.section] = sec
+            data["sections"] = secs
+            tmp = self.path.with_name(f".{self.path.name}.{os.getpid()}.tmp")
+            try:
+                tmp.write_text(json.dumps(data, indent=0, sort_keys=True))
+                os.replace(tmp, self.path)
+            except OSError:
+                try:
+                    tmp.unlink()
+                except OSError:
+                    pass
+                return False
+            self.dirty = False
+            return True
+
+
+def section_for(device, lib_handle) -> str:
+    """Section name: device architecture + CU count + library source hash."""
+    import ctypes
+
+    import torch
+    props = torch.cuda.get_device_properties(device)
+    arch = getattr(props, "gcnArchName", props.name)
+    h = "nohash"
+    if hasattr(lib_handle, "drn_src_hash"):
+        f = lib_handle.drn_src_hash
+        f.restype, f.argtypes = ctypes.c_char_p, []
+        h = f().decode()[:16]
+    return f"{arch}/{props.multi_processor_count}cu|{h}"

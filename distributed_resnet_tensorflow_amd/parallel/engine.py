@@ -87,6 +87,25 @@ def p2p_wanted(allreduce: str, grad_bytes: int, world: int, mode: str = "sync", 
     return grad_bytes <= p2p_max_mb * (1 << 20)
 
 
+def all_ranks_on_one_host(group=None) -> bool:
+    """Whether every rank of `group` runs on this host (a collective: every rank must call it).
+    HIP IPC maps peer buffers only within one node; the launch environment's LOCAL_WORLD_SIZE is
+    set by torchrun and parallel/launch.py but not by --worker_hosts or MPI launches, so the P2P
+    choice is confirmed against the ranks' host identities instead of trusting it."""
+    import socket
+    if dist.get_world_size(group) == 1:
+        return True
+    ident = socket.gethostname()
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            ident += "/" + f.read().strip()
+    except OSError:
+        pass
+    names = [None] * dist.get_world_size(group)
+    dist.all_gather_object(names, ident, group=group)
+    return len(set(names)) == 1
+
+
 class DataParallelEngine:
     def __init__(self, executor, bucket_mb: float = 25.0, mode: str = "sync", group=None,
                  allreduce: str = "rccl", p2p_max_mb: float = 64.0, first_bucket_mb: float = 2.0,
@@ -107,6 +126,8 @@ class DataParallelEngine:
         if self.wire not in ("fp32", "bf16"):
             raise ValueError(f"all-reduce wire type must be fp32 or bf16, got {self.wire!r}")
         want = p2p_wanted(allreduce, self.P.total * 4, self.world, mode, shard_optimizer, p2p_max_mb)
+        if want and allreduce == "auto" and not all_ranks_on_one_host(group):
+            want = False  # (--allreduce=p2p across hosts is refused by the IPC mapping itself)
         if want and self.P.grad.is_cuda and mode == "sync" and self.world <= 8 \
                 and dist.get_backend(group) in ("nccl", "gloo"):
             from .p2p import P2PAllReduce

@@ -33,6 +33,7 @@ Limits: one node, <= 8 ranks, fp32 buckets whose element count is a multiple of 
 from __future__ import annotations
 
 import ctypes
+import logging
 import os
 import pickle
 
@@ -40,6 +41,8 @@ import torch
 import torch.distributed as dist
 
 from ..ops import _lib
+
+log = logging.getLogger("drn")
 
 MAX_RANKS = 8
 N_SLOTS = 64          # ready slots (one per bucket) + the DONE slot 0
@@ -132,7 +135,11 @@ class _DeviceBuffer:
 class P2PAllReduce:
     """Maps every rank's `grad` (and flag words) and reduces buckets of it into `out`."""
 
+    _count = 0
+
     def __init__(self, grad: torch.Tensor, group=None, two_shot_min_kb: int = -1, wire: str = ""):
+        P2PAllReduce._count += 1
+        self._inst = P2PAllReduce._count
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -291,7 +298,29 @@ class P2PAllReduce:
             h.hipIpcCloseMemHandle(ctypes.c_void_p(p))
         self._opened = []
         if self.world > 1:
-            dist.barrier(group=self.group)
+            # time-bounded: a peer that failed (and skipped its close) must not hold this rank in
+            # a collective until the process-group timeout; without the barrier the exported
+            # buffers are left to process exit instead of being freed here
+            try:
+                self._store_barrier(float(os.environ.get("DRN_P2P_CLOSE_TIMEOUT_S", "60")))
+            except Exception as e:  # noqa: BLE001 -- any failure: keep the buffers mapped
+                log.warning("P2P close: peers did not reach the teardown barrier (%s); buffers left to exit", e)
+                self._leaked, self._bufs = self._bufs, []   # (no release: a peer may still map them)
+                return
         for b in self._bufs:
             b.release()
         self._bufs = []
+
+    def _store_barrier(self, timeout_s: float):
+        """A barrier over the process group's TCPStore with a deadline (no collective kernel, so it
+        also works after a device-side failure). Every rank adds 1 to a per-close key and polls."""
+        import time
+        store = dist.distributed_c10d._get_default_store()
+        # (the same key on every rank: instances are created in the same order on all of them)
+        key = f"drn_p2p_close/{self._inst}"
+        store.add(key, 1)
+        deadline = time.monotonic() + timeout_s
+        while int(store.add(key, 0)) < self.world:
+            if time.monotonic() > deadline:
+                raise TimeoutError(f"{key}: {int(store.add(key, 0))}/{self.world} ranks after {timeout_s:.0f} s")
+            time.sleep(0.01)

@@ -895,6 +895,8 @@ class Executor:
         self.P.grad.zero_()
         if self.is_hip:
             torch.cuda.synchronize()
+            if hasattr(self.be, "save_tune_db"):
+                self.be.save_tune_db()   # persist newly timed kernel choices (ops/tunedb.py)
 
     def train_step(self, lr: Optional[float] = None, grad_scale: float = 1.0, allreduce: Optional[Callable] = None):
         if lr is not None:

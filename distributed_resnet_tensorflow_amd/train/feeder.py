@@ -24,6 +24,9 @@ class SyntheticFeeder:
     def next(self):
         return True
 
+    def prefetch(self):
+        pass
+
     def state(self):
         return {}
 
@@ -47,6 +50,13 @@ class _StagedFeeder:
     `state()` is the loader position after the batch most recently handed to the executor (not
     after the batch being prefetched), so a checkpoint resumes with the next unconsumed batch;
     `valid` is that batch's number of real (non-wrapped) images.
+
+    Ordering (reference resnet_cifar_main.py:229-232 overlaps input with compute by
+    `prefetch(2*batch_size)`): `next()` only hands batch k to the executor (stream-ordered
+    preprocess kernel); the host-side load of batch k+1 runs in `prefetch()`, which the training
+    session calls AFTER it has enqueued step k, so the host reads and decodes while the GPU
+    computes. The H2D copies of batch k+1 wait only for the preprocess of batch k (an event), not
+    for the whole step. A caller that never calls `prefetch()` gets it at the next `next()`.
     """
 
     def _init_staging(self, ex):
@@ -54,6 +64,8 @@ class _StagedFeeder:
         self.gpu = ex.device.type == "cuda"
         self.copy_stream = torch.cuda.Stream(device=ex.device) if self.gpu else None
         self._pending = None
+        self._consumed = None          # event after the preprocess of the batch last handed out
+        self._need_prefetch = False
         self._pending_state, self._pending_valid = self.loader.state(), ex.N
         self._state, self.valid = self.loader.state(), ex.N
         self._exhausted = False
@@ -61,7 +73,11 @@ class _StagedFeeder:
     def _stage(self, pairs):
         """pairs: [(device dst, host src)]; enqueues the copies on the copy stream."""
         if self.gpu:
-            self.copy_stream.wait_stream(torch.cuda.current_stream(self.ex.device))
+            # the device staging buffers are free once the previous batch's preprocess has read them
+            if self._consumed is not None:
+                self.copy_stream.wait_event(self._consumed)
+            else:
+                self.copy_stream.wait_stream(torch.cuda.current_stream(self.ex.device))
             with torch.cuda.stream(self.copy_stream):
                 for dst, src in pairs:
                     dst.copy_(_as_tensor(src), non_blocking=True)
@@ -87,13 +103,25 @@ class _StagedFeeder:
             torch.cuda.current_stream(self.ex.device).wait_event(self._pending)
 
     def next(self):
+        if self._need_prefetch:
+            self.prefetch()
         if self._exhausted:
             return False
         self._wait()
         self._consume()
+        if self.gpu:
+            self._consumed = torch.cuda.Event()
+            self._consumed.record(torch.cuda.current_stream(self.ex.device))
         self._state, self.valid = self._pending_state, self._pending_valid
-        self._prefetch()
+        self._need_prefetch = True
         return True
+
+    def prefetch(self):
+        """Host-side load + async H2D staging of the next batch (call after enqueueing the step
+        that consumes the current one)."""
+        if self._need_prefetch:
+            self._need_prefetch = False
+            self._prefetch()
 
     def state(self):
         return dict(self._state)

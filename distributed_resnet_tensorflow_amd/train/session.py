@@ -226,6 +226,11 @@ class TrainingSession:
                 for h in hooks:
                     h.before_step(self, self.global_step)
                 self.step()
+                # the host loads batch k+1 while the GPU runs step k (enqueued above)
+                prefetch = getattr(feeder, "prefetch", None)
+                if prefetch is not None:
+                    with phase("data prefetch"):
+                        prefetch()
                 for h in hooks:
                     h.after_step(self, self.global_step, self.metrics)
         finally:

@@ -1,0 +1,58 @@
+"""Persistent kernel-selection database (ops/tunedb.py): round trip, merge of concurrent writers,
+pruning of stale library sections, and the backend's use of it (a database hit is never re-timed)."""
+import json
+
+from distributed_resnet_tensorflow_amd.ops.tunedb import TuneDB
+
+
+def test_round_trip_and_merge(tmp_path):
+    p = tmp_path / "db.json"
+    a = TuneDB("gfx950/256cu|aaaa", p)
+    a.put_conv((128, 56, 56, 64, 64, 3, 3, 56, 56, 1, 1, 1, 1, True, 0, False, False, True, False), (25, -512))
+    a.put_wgrad((128, 56, 56, 64, 64, 3, 3, 56, 56, 1, 1, 1, True, False), (512, 7, True, 8))
+    assert a.save() and not a.dirty
+    assert not a.save()                      # nothing new: no write
+    b = TuneDB("gfx950/256cu|aaaa", p)       # a second process of the same library
+    assert b.get_conv((128, 56, 56, 64, 64, 3, 3, 56, 56, 1, 1, 1, 1, True, 0, False, False, True, False)) == (25, -512)
+    assert b.get_wgrad((128, 56, 56, 64, 64, 3, 3, 56, 56, 1, 1, 1, True, False)) == (512, 7, True, 8)
+    assert b.get_conv((1, 2, 3)) is None
+    b.put_conv((1, 2, 3), (0, 1))
+    a.put_conv((4, 5, 6), (3, 2))            # concurrent writer: both keys survive
+    b.save()
+    a.save()
+    c = TuneDB("gfx950/256cu|aaaa", p)
+    assert c.get_conv((1, 2, 3)) == (0, 1) and c.get_conv((4, 5, 6)) == (3, 2)
+
+
+def test_stale_library_sections_are_dropped(tmp_path):
+    p = tmp_path / "db.json"
+    old = TuneDB("gfx950/256cu|old0", p)
+    old.put_conv((1,), (1, 1))
+    old.save()
+    other_dev = TuneDB("gfx942/304cu|old0", p)
+    other_dev.put_conv((1,), (2, 1))
+    other_dev.save()
+    new = TuneDB("gfx950/256cu|new0", p)
+    assert new.get_conv((1,)) is None         # another library build: never reused
+    new.put_conv((1,), (5, 1))
+    new.save()
+    secs = json.loads(p.read_text())["sections"]
+    assert set(secs) == {"gfx950/256cu|new0", "gfx942/304cu|old0"}
+
+
+def test_version_mismatch_and_corrupt_file_are_ignored(tmp_path):
+    p = tmp_path / "db.json"
+    p.write_text(json.dumps({"version": 999, "sections": {"s|h": {"conv": {"1": [7, 1]}}}}))
+    assert TuneDB("s|h", p).get_conv((1,)) is None
+    p.write_text("{not json")
+    db = TuneDB("s|h", p)
+    assert db.get_conv((1,)) is None
+    db.put_conv((1,), (3, 1))
+    assert db.save() and TuneDB("s|h", p).get_conv((1,)) == (3, 1)
+
+
+def test_disabled_by_env(tmp_path, monkeypatch):
+    monkeypatch.setenv("DRN_TUNE_DB", "off")
+    db = TuneDB("s|h")
+    db.put_conv((1,), (3, 1))
+    assert db.path is None and not db.save()
