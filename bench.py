@@ -52,6 +52,11 @@ def main():
     ap.add_argument("--allreduce_wire", default="fp32", choices=["fp32", "bf16"],
                     help="gradient dtype on the wire (bf16: half the all-reduce bytes)")
     args = ap.parse_args()
+    # the result line is the ONLY thing on stdout: libraries that print banners there (RCCL's
+    # version block at communicator init) are sent to stderr at the file-descriptor level
+    sys.stdout.flush()
+    result_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
 
     import torch
     import torch.distributed as dist
@@ -208,7 +213,8 @@ def main():
         if args.width > 1:
             model = f"wide_resnet{args.resnet_size}_{args.width}_{args.dataset}"
         out = {
-            "metric": "images/sec (whole node) ResNet-50 bs=128/GPU" if (args.width == 1 and args.batch_size == 128)
+            "metric": "images/sec (whole node) ResNet-50 bs=128/GPU"
+            if (args.dataset == "imagenet" and args.resnet_size == 50 and args.width == 1 and args.batch_size == 128)
             else f"images/sec (whole node) {model} bs={args.batch_size}/GPU",
             "value": round(img_s, 2),
             "unit": "images/sec",
@@ -227,7 +233,7 @@ def main():
                        "parallelism": f"dp{world}", "hip_graph": bool(use_graph)},
             "final_loss": round(loss, 4),
         }
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=result_out, flush=True)
     if os.environ.get("DRN_PRINT_TUNE") == "1" and rank == 0:
         for key, cfg, us in be.tune_log:
             print(f"[tune] {key} -> {cfg} ({us} us)", file=sys.stderr)

@@ -1,0 +1,147 @@
+"""Bench-geometry correctness: every distinct convolution of the ResNet-50 v2 training step at the
+benchmark shape (batch 128, 224 x 224) runs with the kernel configuration the
+autotuner (or the tuning database) chose for it -- forward and data-gradient launches including
+split-K / stream-K / halo tiles, and weight-gradient launches with their split counts -- and is
+compared with the fp32 reference of the same op (ops.backend.RefBackend on the GPU: test oracle
+only) on fresh bf16-rounded random operands.
+
+The launches are recorded from one real autotuned forward + backward of the executor, so the test
+covers exactly the (geometry, configuration) pairs bench.py times."""
+import ctypes
+
+import pytest
+import torch
+
+from distributed_resnet_tensorflow_amd.models.spec import build_spec
+from distributed_resnet_tensorflow_amd.ops.backend import ConvGeom, HipBackend, OutMap, RefBackend
+from distributed_resnet_tensorflow_amd.runtime.executor import Executor
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")]
+
+BATCH = 128
+_REC = {}
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+def _record():
+    """One autotuned ResNet-50 step; returns {key: ('fwd', args copy)} and {key: ('wgrad', ...)}."""
+    if _REC:
+        return _REC
+    be = HipBackend("cuda")
+    ex = Executor(build_spec("imagenet", 50), BATCH, be, "cuda", seed=0, weight_decay=1e-4)
+    be.synthetic_images(ex.images, seed=3)
+    ex.autotune()
+    fwd, wg = {}, {}
+    launch, wgrad = be.launch_conv, be.conv_wgrad
+
+    def rec_launch(a):
+        key = be.conv_key(a)
+        if key not in fwd:
+            c = type(a)()
+            ctypes.memmove(ctypes.addressof(c), ctypes.addressof(a), ctypes.sizeof(a))
+            fwd[key] = c
+        return launch(a)
+
+    def rec_wgrad(x, dy, out, g, in_bn=None, relu_in=True, ws=None, bnb=None):
+        k = (tuple(x.shape), tuple(dy.shape), tuple(out.shape), g.stride, g.pad_h, g.pad_w, in_bn is not None,
+             bnb is not None)
+        wg.setdefault(k, (g, relu_in))
+        return wgrad(x, dy, out, g, in_bn=in_bn, relu_in=relu_in, ws=ws, bnb=bnb)
+
+    be.launch_conv, be.conv_wgrad = rec_launch, rec_wgrad
+    ex.forward(train=True)
+    ex.backward()
+    torch.cuda.synchronize()
+    be.launch_conv, be.conv_wgrad = launch, wgrad
+    _REC.update(be=be, ex=ex, fwd=fwd, wgrad=wg)
+    return _REC
+
+
+N_SLOTS = 96  # parametrised slots per kind (the launches themselves are recorded on the GPU box)
+
+
+def test_bench_geometry_slots_cover_every_launch():
+    r = _record()
+    assert 0 < len(r["fwd"]) <= N_SLOTS and 0 < len(r["wgrad"]) <= N_SLOTS, (len(r["fwd"]), len(r["wgrad"]))
+
+
+@pytest.mark.parametrize("i", list(range(N_SLOTS)))
+def test_bench_geometry_conv(i):
+    r = _record()
+    be, keys = r["be"], sorted(r["fwd"], key=str)
+    if i >= len(keys):
+        pytest.skip("fewer distinct conv launches than parametrised slots")
+    a0 = r["fwd"][keys[i]]
+    N, H, W, C, K, R, S, P, Q = a0.N, a0.H, a0.W, a0.C, a0.K, a0.R, a0.S, a0.P, a0.Q
+    torch.manual_seed(i)
+    dev = "cuda"
+    C_store = C
+    x = torch.randn(N, H, W, C_store, device=dev).bfloat16()
+    if C == 4:  # packed stem input: 4 channels, the 4th a zero pad (RGB)
+        x[..., 3] = 0
+    w = (torch.randn(K, R, S, C_store, device=dev) * (2.0 / (R * S * C_store)) ** 0.5).bfloat16()
+    mapped = a0.out_stride != 0
+    oH, oW = (a0.out_H, a0.out_W) if mapped else (P, Q)
+    om = OutMap(P, Q, a0.out_stride, a0.out_oh, a0.out_ow) if mapped else None
+    g = ConvGeom(a0.stride, a0.pad_h, a0.pad_w, a0.dil)
+    in_bn = (torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.3) if a0.in_scale else None
+    res = torch.randn(N, oH, oW, K, device=dev).bfloat16() if a0.residual else None
+    bb = None
+    if a0.bn_x:
+        bb = (torch.randn(N, oH, oW, K, device=dev).bfloat16(), torch.rand(K, device=dev) + 0.5,
+              torch.randn(K, device=dev) * 0.3, torch.randn(K, device=dev) * 0.1, torch.rand(K, device=dev) + 0.5)
+    rep = max(1, a0.stats_rep)
+    st = torch.zeros(rep, 2, K, device=dev) if a0.stats else None
+    y = torch.zeros(N, oH, oW, K, device=dev, dtype=torch.bfloat16)
+    if res is not None and mapped:
+        y.copy_(res)            # accumulating phase launch: residual == output
+        res = y
+    a = be.conv_args(x, w, y, g, in_bn=in_bn, residual=res, stats=st, out_map=om, bn_bwd=bb)
+    assert be.conv_key(a) == keys[i]
+    cfg = be.conv_cfg.get(keys[i])
+    assert cfg is not None, "the benchmark launch was not tuned"
+    res_ref = None if res is None else res.float().clone()
+    be.launch_conv(a)
+    torch.cuda.synchronize()
+    ref = RefBackend(dev)
+    y_ref = torch.zeros(N, oH, oW, K, device=dev)
+    if res_ref is not None and mapped:
+        y_ref.copy_(res_ref)
+    st_ref = torch.zeros(2 * K, device=dev) if st is not None else None
+    ref.conv_fwd(x.float(), w.float(), y_ref, g, in_bn=in_bn, residual=res_ref, stats=st_ref, out_map=om,
+                 bn_bwd=None if bb is None else (bb[0].float(),) + bb[1:])
+    assert _rel(y, y_ref) < 1e-2, (keys[i], cfg)
+    if st is not None:
+        s = st.sum(0).view(-1)
+        tol = 3e-2 if bb is not None else 2e-2
+        assert _rel(s[:K], st_ref[:K]) < tol and _rel(s[K:], st_ref[K:]) < tol, (keys[i], cfg)
+
+
+@pytest.mark.parametrize("i", list(range(N_SLOTS)))
+def test_bench_geometry_wgrad(i):
+    r = _record()
+    be, ex = r["be"], r["ex"]
+    keys = sorted(r["wgrad"], key=str)
+    if i >= len(keys):
+        pytest.skip("fewer distinct weight-gradient launches than parametrised slots")
+    k = keys[i]
+    xs, dys, outs, _, _, _, pro, bnb = k
+    if bnb:
+        pytest.skip("BN-backward dY prologue (off by default)")
+    g, relu_in = r["wgrad"][k]
+    torch.manual_seed(1000 + i)
+    dev = "cuda"
+    x = torch.randn(*xs, device=dev).bfloat16()
+    dy = torch.randn(*dys, device=dev).bfloat16()
+    C = xs[-1]
+    in_bn = (torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.3) if pro else None
+    out = torch.zeros(*outs, device=dev)
+    be.conv_wgrad(x, dy, out, g, in_bn=in_bn, relu_in=relu_in, ws=ex.wgrad_ws)
+    torch.cuda.synchronize()
+    out_ref = torch.zeros(*outs, device=dev)
+    RefBackend(dev).conv_wgrad(x.float(), dy.float(), out_ref, g, in_bn=in_bn, relu_in=relu_in)
+    assert _rel(out, out_ref) < 1e-2, (k, be.wgrad_ns.get(be.wgrad_key(be.wgrad_args(x, dy, out, g, in_bn))))
