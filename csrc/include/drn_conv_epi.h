@@ -170,12 +170,20 @@ __device__ __forceinline__ int epi_off(const DrnConvFwdArgs& a, int m, int c, in
   return ((n * a.out_H + i * a.out_stride + a.out_oh) * a.out_W + j * a.out_stride + a.out_ow) * a.K + c;
 }
 
+// Row map of the staged tile: staged row -> output pixel m (>= M: not an output pixel). The
+// implicit-GEMM kernels' tiles are consecutive pixels; the halo kernel's rows are 16-pixel
+// fragments of image rows (conv_halo.hip EpiRowHalo).
+struct EpiRowId {
+  __device__ __forceinline__ int operator()(int m0, int row) const { return m0 + row; }
+};
+
 // LAZY: output offsets computed per row here instead of held in e.off (no registers across the
 // main loop / the other slices)
-template <int BP, int BC, int WP, int MI, int MJ, int NT = 256, bool PF = true, bool LAZY = false>
+template <int BP, int BC, int WP, int MI, int MJ, int NT = 256, bool PF = true, bool LAZY = false,
+          typename RM = EpiRowId>
 __device__ __forceinline__ void conv_epilogue_pass(const DrnConvFwdArgs& a, char* smem, f32x4_t (&acc)[MI][MJ],
                                                    bool stage, int wp, int wcs, int m0, int c0, int M,
-                                                   const EpiPre<BP, BC, NT, PF>& e) {
+                                                   const EpiPre<BP, BC, NT, PF>& e, RM rmap = RM()) {
   static_assert(!(LAZY && PF), "lazy offsets: no prefetched operands");
   using E = EpiPre<BP, BC, NT, PF>;
   const int tid = threadIdx.x;
@@ -221,7 +229,7 @@ __device__ __forceinline__ void conv_epilogue_pass(const DrnConvFwdArgs& a, char
     const int row = it * RPI + tid / CHR;
     const f32x4_t lo = *reinterpret_cast<const f32x4_t*>(tile + row * BC + (((2 * ch) ^ (row & SWM)) * 4));
     const f32x4_t hi = *reinterpret_cast<const f32x4_t*>(tile + row * BC + (((2 * ch + 1) ^ (row & SWM)) * 4));
-    const int off = LAZY ? epi_off(a, m0 + row, c, M) : e.off[it];
+    const int off = LAZY ? epi_off(a, rmap(m0, row), c, M) : e.off[it];
     if (off >= 0) {
       float f[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       if (has_res) {
@@ -251,7 +259,7 @@ __device__ __forceinline__ void conv_epilogue_pass(const DrnConvFwdArgs& a, char
         *reinterpret_cast<uint4*>(y + off) = o;
         if (a.out_fill && a.out_stride > 1) {
           // zeros at this pixel's sibling phase positions (single-phase strided output)
-          const int m = m0 + row;
+          const int m = rmap(m0, row);
           const int pq = a.P * a.Q;
           const int n = (int)drn_fdiv((uint32_t)m, a.fd_pq);
           const int rem = m - n * pq;
@@ -316,9 +324,9 @@ __device__ __forceinline__ void conv_epilogue(const DrnConvFwdArgs& a, char* sme
 
 // NH channel slices of BC / NH (each wave's WC channels lie inside one slice); no prefetched
 // epilogue operands (the big tiles spend their registers on accumulators)
-template <int BP, int BC, int WP, int WC, int MI, int MJ, int NT, int NH>
+template <int BP, int BC, int WP, int WC, int MI, int MJ, int NT, int NH, typename RM = EpiRowId>
 __device__ __forceinline__ void conv_epilogue_sliced(const DrnConvFwdArgs& a, char* smem, f32x4_t (&acc)[MI][MJ],
-                                                     int wp, int wc, int m0, int c0, int M) {
+                                                     int wp, int wc, int m0, int c0, int M, RM rmap = RM()) {
   constexpr int BCH = BC / NH;
   static_assert(BC % NH == 0 && BCH % WC == 0, "a wave's channels must lie inside one slice");
 #pragma unroll 1
@@ -326,8 +334,8 @@ __device__ __forceinline__ void conv_epilogue_sliced(const DrnConvFwdArgs& a, ch
     if (h > 0) __syncthreads();  // the previous slice's LDS reads / reductions are done
     EpiPre<BP, BCH, NT, false> e;  // unused (LAZY offsets)
     const int wcs = wc * WC - h * BCH;
-    conv_epilogue_pass<BP, BCH, WP, MI, MJ, NT, false, true>(a, smem, acc, wcs >= 0 && wcs < BCH, wp, wcs, m0,
-                                                             c0 + h * BCH, M, e);
+    conv_epilogue_pass<BP, BCH, WP, MI, MJ, NT, false, true, RM>(a, smem, acc, wcs >= 0 && wcs < BCH, wp, wcs, m0,
+                                                                 c0 + h * BCH, M, e, rmap);
   }
   if (a.stats != nullptr && a.fin_cnt != nullptr) bn_fin_column<BP, BC, NT>(a, c0, M, reinterpret_cast<int*>(smem));
 }

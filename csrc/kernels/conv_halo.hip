@@ -5,8 +5,8 @@
 // then does 64 FLOP per staged byte, and at the ~70 GB/s a CU draws from L2 the MFMA pipe runs
 // at <= ~45 % (measured: the ResNet-50 3x3 layers at 500-650 TF/s, profiles/r4_*).
 //
-// Here a workgroup owns a SPATIAL output tile -- `th` whole output rows of one image, or `ni`
-// whole images when an image is small (14x14, 7x7) -- times BC output channels. Per 64-channel
+// Here a workgroup owns a SPATIAL output tile -- `th` whole output rows of one image -- times BC
+// output channels. Per 64-channel
 // input chunk the tile's input HALO ((th + R - 1) x (W + S - 1) pixels per image, zero padded)
 // is staged ONCE into LDS by LDS-DMA, and all R*S taps read their B fragments from it at a
 // uniform tap offset; only the weights [BC][64] of each (chunk, tap) step stream through a ring
@@ -21,27 +21,50 @@
 //
 // Layout: 8 waves = WAVES_P (pixel groups of MJ 16-pixel fragments) x WAVES_C (channel groups of
 // MI 16-channel fragments); MFMA v_mfma_f32_16x16x32_bf16, A = weights (rows = output channels),
-// B = halo pixels. LDS rows are 128 B (64 channels) with 16-byte slots XOR-swizzled by
-// (row >> 1) & 7 (glds_swz<64>, conflict-free ds_read_b128 fragment reads); the swizzle is
-// applied on the per-lane SOURCE address of the lane-linear LDS-DMA.
+// B = halo pixels. LDS rows are 128 B (64 channels) with 16-byte slots XOR-swizzled (weights:
+// (row >> 1) & 7 = glds_swz<64>, halo: halo_swz), both conflict-free for the ds_read_b128 fragment
+// reads; the swizzle is applied on the per-lane SOURCE address of the lane-linear LDS-DMA.
 #include "drn_common.h"
 #include "drn_conv.h"
 #include "drn_conv_epi.h"
 
 namespace drn {
 
-// Host-computed tile geometry (one launch).
+// Host-computed tile geometry (one launch). A tile is `th` output rows of one image; every row is
+// cut into fpr 16-pixel fragments (the last one partly past the row end: garbage columns that are
+// computed and never stored). A fragment therefore never wraps to the next row, so its 16 lanes
+// read 16 CONSECUTIVE halo pixels at every tap, which halo_swz spreads over all 16-byte slots of
+// a bank row (conflict-free ds_read_b128). Fragments wrapping an image row measured 39 % LDS bank
+// conflicts, 16-pixel runs with the (row >> 1) & 7 swizzle 33 % (runs start unaligned).
 struct HaloGeom {
-  int32_t ni, th;        // images per tile (whole images when > 1), output rows per tile
-  int32_t tpi;           // tiles per image (ni == 1) = P / th
-  int32_t hh, hw;        // halo rows per image segment (th + R - 1), halo columns (Q + S - 1)
-  int32_t hpx;           // halo pixels of a tile = ni * hh * hw
-  int32_t tp;            // output pixels of a tile = ni * th * Q
-  int32_t ntp;           // pixel tiles
+  int32_t th;            // output rows per tile
+  int32_t tpi;           // tiles per image = P / th
+  int32_t fpr;           // 16-pixel fragments per output row = ceil(Q / 16)
+  int32_t hh, hw;        // halo rows (th + R - 1), halo columns (Q + S - 1)
+  int32_t hpx;           // halo pixels of a tile = hh * hw
+  int32_t ntp;           // pixel tiles = N * tpi
 };
 
-// s_waitcnt vmcnt(n) for a run-time n (0..63): one scalar branch per step
-__device__ __forceinline__ void wait_vmcnt_rt(int n) {
+// staged epilogue row -> output pixel (>= M for garbage columns / fragments past the tile)
+struct EpiRowHalo {
+  int fpr, Q, th, M;
+  __device__ __forceinline__ int operator()(int m0, int row) const {
+    const int f = row >> 4;
+    const int r = f / fpr;
+    const int c = (f - r * fpr) * 16 + (row & 15);
+    return (r < th && c < Q) ? m0 + r * Q + c : M;
+  }
+};
+
+// 16-byte slot swizzle of the halo image: logical chunk c of halo pixel hp sits in slot
+// c ^ (hp & 6). Unlike the (hp >> 1) & 7 swizzle of the implicit-GEMM tiles (conflict-free only
+// for 16-aligned row groups), it keeps ds_read_b128 conflict-free for a fragment's 16 consecutive
+// halo pixels at ANY start (a tap shifts the run by dr * hw + ds): exhaustive check over the four
+// gfx950 lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31}, ... and both k halves.
+__device__ __forceinline__ int halo_swz(int hp) { return hp & 6; }
+
+// s_waitcnt vmcnt(n) for a run-time n (0..30), off the steady-state path
+__device__ __noinline__ void wait_vmcnt_rt(int n) {
   switch (n) {
 #define DRN_W(k) \
   case k:        \
@@ -57,24 +80,26 @@ __device__ __forceinline__ void wait_vmcnt_rt(int n) {
 }
 
 // MJ pixel fragments per wave; HPW = max halo pieces (8 pixels x 128 B each) per wave
-template <int WAVES_P, int MJ, int WAVES_C, int MI, int D, int HPW>
+template <int WAVES_P, int MJ, int WAVES_C, int MI, int D, int HPW, bool PRO>
 __global__ __launch_bounds__(512) void conv_halo_kernel(DrnConvFwdArgs a, HaloGeom g, const void* __restrict__ zero) {
   constexpr int NW = 8, NT = 512;
   static_assert(WAVES_P * WAVES_C == NW, "8 waves");
-  constexpr int BP = WAVES_P * MJ * 16;   // computed pixel columns (>= g.tp)
+  constexpr int BP = WAVES_P * MJ * 16;   // computed pixel columns (th * fpr * 16 <= BP)
   constexpr int BC = WAVES_C * MI * 16;   // output channels per tile
   constexpr int WP = MJ * 16, WC = MI * 16;
   constexpr int NWB = D + 1;              // weight ring buffers
   constexpr int GW = BC / 64;             // weight glds pieces per wave per step (BC rows x 128 B / 8 waves)
+  constexpr int STEADY = (D - 1) * GW;    // loads left in flight at a steady-state step
   static_assert(GW >= 1 && GW * 64 == BC, "BC multiple of 64");
-  static_assert(BP % (NT / ((BC > 128 ? 128 : BC) / 8)) == 0, "the epilogue's row groups must tile BP");
+  static_assert(HPW % 4 == 0, "halo pieces per wave: batches of 4");
+  static_assert(D >= 2 && STEADY < 31, "pipeline depth");
   extern __shared__ __attribute__((aligned(1024))) char smem[];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int C = a.C, K = a.K, R = a.R, S = a.S;
-  const int RS = R * S;
+  const int C = a.C, K = a.K, S = a.S;
+  const int RS = a.R * S;
   const int nchunk = C >> 6;
   const int T = nchunk * RS;              // steps (chunk-major, tap-minor)
   const int M = a.N * a.P * a.Q;
@@ -82,45 +107,34 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(DrnConvFwdArgs a, HaloGe
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tcol = bid % ntc, tpix = bid / ntc;
   const int c0 = tcol * BC;
-  // spatial tile -> first image / first output row, first output pixel
-  int n0, p0;
-  if (g.ni > 1) {
-    n0 = tpix * g.ni;
-    p0 = 0;
-  } else {
-    n0 = tpix / g.tpi;
-    p0 = (tpix - n0 * g.tpi) * g.th;
-  }
+  const int n0 = tpix / g.tpi;
+  const int p0 = (tpix - n0 * g.tpi) * g.th;
   const int m0 = (n0 * a.P + p0) * a.Q;
-  const int m_end = min(m0 + g.tp, M);
 
-  // LDS: [halo buffer 0][halo buffer 1 (nchunk > 1)][NWB weight buffers][...]
-  const int hbytes = ((g.hpx + 7) >> 3) << 10;  // rounded up to whole 8-pixel pieces
-  char* const hbuf0 = smem;
+  // LDS: [halo buffer 0][halo buffer 1 (nchunk > 1)][NWB weight buffers][PRO: scale C, shift C];
+  // a halo buffer holds the tile's halo plus 2 spare KB read by the garbage columns of the last
+  // fragment of a row
+  const int npieces = (g.hpx + 7) >> 3;
+  const int hbytes = (npieces + 2) << 10;
   char* const wbuf0 = smem + (nchunk > 1 ? 2 : 1) * hbytes;
   constexpr int WBYTES = BC * 128;
+  float* const ssl = reinterpret_cast<float*>(wbuf0 + NWB * WBYTES);
 
   // ---- halo loader: per-lane source offsets of this wave's pieces (element offset at chunk 0,
   // -1 = outside the image: the zero page) ----
-  const int npieces = (g.hpx + 7) >> 3;
   const int my_pieces = npieces > wave ? (npieces - wave + NW - 1) / NW : 0;  // wave-uniform
   int hoff[HPW];
-  const int hslot = lane & 7;
 #pragma unroll
   for (int i = 0; i < HPW; ++i) {
     const int hp = (i * NW + wave) * 8 + (lane >> 3);
     int off = -1;
     if (i < my_pieces && hp < g.hpx) {
-      const int seg = g.hh * g.hw;
-      const int img = hp / seg;
-      const int rem = hp - img * seg;
-      const int ar = rem / g.hw;
-      const int bc = rem - ar * g.hw;
-      const int n = n0 + img;
+      const int ar = hp / g.hw;
+      const int bc = hp - ar * g.hw;
       const int h = p0 - a.pad_h + ar;
       const int w = bc - a.pad_w;
-      if (n < a.N && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
-        off = ((n * a.H + h) * a.W + w) * C + ((hslot ^ glds_swz<64>(hp)) << 3);
+      if ((unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W)
+        off = ((n0 * a.H + h) * a.W + w) * C + (((lane & 7) ^ halo_swz(hp)) << 3);
     }
     hoff[i] = off;
   }
@@ -135,48 +149,36 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(DrnConvFwdArgs a, HaloGe
     }
   };
   // ---- weight loader: rows c0 + row of w[K][R][S][C], 64 channels of one (tap, chunk) ----
-  const int Ktot = RS * C;
-  const bf16_t* __restrict__ wg = reinterpret_cast<const bf16_t*>(a.w);
-  uint32_t woff[GW];
-#pragma unroll
-  for (int i = 0; i < GW; ++i) {
-    const int row = (i * NW + wave) * 8 + (lane >> 3);
-    woff[i] = (uint32_t)((c0 + row) * Ktot + (((lane & 7) ^ glds_swz<64>(row)) << 3));
+  const bf16_t* __restrict__ wrow;
+  {
+    const int row = wave * 8 + (lane >> 3);  // + i * 64 rows for piece i
+    wrow = reinterpret_cast<const bf16_t*>(a.w) + (size_t)(c0 + row) * (RS * C) + (((lane & 7) ^ glds_swz<64>(row)) << 3);
   }
-  auto issue_w = [&](int step) {
-    const int chunk = step / RS, tap = step - chunk * RS;
-    const bf16_t* __restrict__ ws = wg + tap * C + (chunk << 6);
-    char* wb = wbuf0 + (step % NWB) * WBYTES;
+  const size_t wpiece = (size_t)64 * RS * C;  // 64 rows further (the swizzle bits repeat every 16 rows)
+  auto issue_w = [&](int koff, int slot) {   // koff = tap * C + chunk * 64
+    char* wb = wbuf0 + slot * WBYTES;
 #pragma unroll
-    for (int i = 0; i < GW; ++i) glds16(ws + woff[i], wb + ((i * NW + wave) << 10));
+    for (int i = 0; i < GW; ++i) glds16(wrow + i * wpiece + koff, wb + ((i * NW + wave) << 10));
   };
 
   // ---- fragment addressing ----
   const int wp = wave % WAVES_P, wc = wave / WAVES_P;
   const int fr = lane & 15, fk = lane >> 4;
-  // B: output pixel o of the tile -> halo pixel of tap (0, 0); padded columns read pixel 0
+  // B: fragment f = (row f / fpr, columns (f % fpr) * 16 ..) -> halo pixel of tap (0, 0)
   int hb0[MJ];
 #pragma unroll
   for (int j = 0; j < MJ; ++j) {
-    const int o = (wp * MJ + j) * 16 + fr;
-    int hp = 0;
-    if (o < g.tp) {
-      const int per_img = g.th * a.Q;
-      const int img = o / per_img;
-      const int rem = o - img * per_img;
-      const int r = rem / a.Q;
-      const int c = rem - r * a.Q;
-      hp = (img * g.hh + r) * g.hw + c;
-    }
-    hb0[j] = hp;
+    const int f = wp * MJ + j;
+    const int r = f / g.fpr;
+    const int c = (f - r * g.fpr) * 16 + fr;
+    hb0[j] = (r < g.th ? r : 0) * g.hw + c;  // (fragments past the tile read row 0: garbage, not stored)
   }
   uint32_t aoff[MI];
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int row = wc * WC + i * 16 + fr;  // 16-aligned groups: the swizzle bits are fr's
-    aoff[i] = (uint32_t)(row * 128);
+    aoff[i] = (uint32_t)(row * 128 + ((fk ^ glds_swz<64>(fr)) << 4));
   }
-  const int aswz = glds_swz<64>(fr);
 
   f32x4_t acc[MI][MJ];
 #pragma unroll
@@ -184,64 +186,180 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(DrnConvFwdArgs a, HaloGe
 #pragma unroll
     for (int j = 0; j < MJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // ---- prologue: halo of chunk 0, weights of steps 0 .. D-1 ----
-  issue_halo(0, hbuf0);
+  // ---- prologue: halo of chunk 0, weights of steps 0 .. D-1 (tap-minor k offsets) ----
+  issue_halo(0, smem);
+  // PRO: the input is the raw pre-BN tensor; relu(x * scale + shift) is applied to the halo ONCE
+  // per chunk in LDS (each lane rewrites the 16-byte pieces its own LDS-DMAs landed, before the
+  // chunk's first barrier; zero-padding pieces stay zero) -- 1/(R*S) of the per-tap rewrite an
+  // im2col tile needs. scale / shift of every channel are staged in LDS behind the buffers (or
+  // finalized there from the BN statistics: consumer-side finalize, DrnBnFin).
+  if constexpr (PRO) {
+    if (a.in_fin.stats != nullptr) {
+      const bool pub = a.in_fin.publish && blockIdx.x == 0;
+      for (int c = tid; c < C; c += NT) drn_bn_fin_fwd(a.in_fin, c, pub, ssl[c], ssl[C + c]);
+    } else {
+      for (int c = tid; c < C; c += NT) {
+        ssl[c] = a.in_scale[c];
+        ssl[C + c] = a.in_shift[c];
+      }
+    }
+    __syncthreads();
+  }
+  // the lane's logical chunk inside a halo piece: (lane & 7) ^ halo_swz(hp) with hp & 6 = the
+  // bits 1-2 of lane >> 3 for every piece (pieces are 8-pixel aligned)
+  const int plc = (lane & 7) ^ halo_swz(lane >> 3);
+  auto transform_halo = [&](int chunk, char* hb) {
+    const uint32_t sp = lds_addr(ssl + (chunk << 6) + plc * 8);
+    u32x4_t q[4];
+    q[0] = lds_read16(sp);
+    q[1] = lds_read16(sp + 16);
+    q[2] = lds_read16(sp + 4 * C);
+    q[3] = lds_read16(sp + 4 * C + 16);
+    lds_wait_all<4>(q);
+    f32x2_t sc2[4], sh2[4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      sc2[2 * k] = f32x2_t{__uint_as_float(q[k][0]), __uint_as_float(q[k][1])};
+      sc2[2 * k + 1] = f32x2_t{__uint_as_float(q[k][2]), __uint_as_float(q[k][3])};
+      sh2[2 * k] = f32x2_t{__uint_as_float(q[2 + k][0]), __uint_as_float(q[2 + k][1])};
+      sh2[2 * k + 1] = f32x2_t{__uint_as_float(q[2 + k][2]), __uint_as_float(q[2 + k][3])};
+    }
+    // in batches of 4 pieces (registers: the accumulators and prefetched fragments are live)
+#pragma unroll
+    for (int i0 = 0; i0 < HPW; i0 += 4) {
+      u32x4_t v[4];
+      uint32_t pa[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        pa[k] = lds_addr(hb + (((i0 + k) * NW + wave) << 10) + lane * 16);
+        if (i0 + k < my_pieces) v[k] = lds_read16(pa[k]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (i0 + k < my_pieces) {
+          u32x4_t o = bn_relu_piece<true>(v[k], sc2, sh2);
+          const unsigned m = hoff[i0 + k] >= 0 ? 0xffffffffu : 0u;  // zero-page pieces stay zero
+          o.x &= m;
+          o.y &= m;
+          o.z &= m;
+          o.w &= m;
+          lds_write16(pa[k], o);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  int wtap = 0, wchunk = 0, wslot = 0, wstep = 0;
+  auto issue_next_w = [&]() {
+    issue_w(wtap * C + (wchunk << 6), wslot);
+    if (++wtap == RS) {
+      wtap = 0;
+      ++wchunk;
+    }
+    wslot = wslot + 1 == NWB ? 0 : wslot + 1;
+    ++wstep;
+  };
 #pragma unroll
   for (int s = 0; s < D; ++s)
-    if (s < T) issue_w(s);
+    if (wstep < T) issue_next_w();
 
   const uint32_t lds0 = lds_addr(smem);
+  const uint32_t wlds0 = lds0 + (uint32_t)(wbuf0 - smem);
+  int tap = 0, chunk = 0, dr = 0, ds = 0, cslot = 0;
+  u32x4_t bv[2][MJ];  // this step's B fragments (k halves 0, 1)
   for (int s = 0; s < T; ++s) {
-    const int chunk = s / RS, tap = s - chunk * RS;
     // loads allowed to stay in flight: the weights of steps s+1 .. s+D-1, plus the halo batch of
-    // the next chunk when it was issued after W(s) (at step chunk*RS, s within D-1 steps of it)
-    const int ahead = min(D - 1, T - 1 - s);
-    int allowed = ahead * GW;
-    const int hs = chunk * RS;  // step that issued the halo batch of chunk + 1
-    if (chunk + 1 < nchunk && s > hs && s - hs <= D - 1) allowed += my_pieces;  // (R*S >= D: one batch at most)
-    wait_vmcnt_rt(allowed);
+    // the next chunk when it was issued after W(s) (at the chunk's first step, < D steps ago;
+    // R*S >= D: at most one batch)
+    const int ahead = T - 1 - s < D - 1 ? T - 1 - s : D - 1;
+    const int allowed = ahead * GW + ((chunk + 1 < nchunk && tap >= 1 && tap <= D - 1) ? my_pieces : 0);
+    if (allowed == STEADY) wait_vmcnt<STEADY>();
+    else wait_vmcnt_rt(allowed);
+    if constexpr (PRO) {
+      if (tap == 0) transform_halo(chunk, smem + (chunk & 1) * hbytes);  // this chunk's halo landed
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (tap == 0 && chunk + 1 < nchunk) issue_halo(chunk + 1, hbuf0 + ((chunk + 1) & 1) * hbytes);
-    if (s + D < T) issue_w(s + D);
-    // tap offset inside the halo
-    const int dr = tap / S, ds = tap - dr * S;
-    const int toff = dr * g.hw + ds;
+    if (tap == 0 && chunk + 1 < nchunk) issue_halo(chunk + 1, smem + ((chunk + 1) & 1) * hbytes);
+    if (wstep < T) issue_next_w();
     const uint32_t hbase = lds0 + (uint32_t)((chunk & 1) * hbytes);
-    const uint32_t wbase = lds0 + (uint32_t)(wbuf0 - smem) + (uint32_t)((s % NWB) * WBYTES);
-#pragma unroll
-    for (int kh = 0; kh < 2; ++kh) {
-      const int c16 = kh * 4 + fk;
-      bf16x8_t af[MI], bfr[MJ];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const u32x4_t v = lds_read16(wbase + aoff[i] + (uint32_t)((c16 ^ aswz) << 4));
-        af[i] = __builtin_bit_cast(bf16x8_t, v);
-      }
+    const uint32_t wbase = wlds0 + (uint32_t)(cslot * WBYTES);
+    // B fragments of this step: prefetched during the previous step when it was in the same
+    // chunk (the halo buffer is stable for a whole chunk), else read now
+    if (tap == 0) {
+      const int toff = dr * g.hw + ds;
 #pragma unroll
       for (int j = 0; j < MJ; ++j) {
         const int hp = hb0[j] + toff;
-        const u32x4_t v = lds_read16(hbase + (uint32_t)(hp << 7) + (uint32_t)((c16 ^ glds_swz<64>(hp)) << 4));
-        bfr[j] = __builtin_bit_cast(bf16x8_t, v);
+        const uint32_t ad = hbase + (uint32_t)(hp << 7) + (uint32_t)((fk ^ halo_swz(hp)) << 4);
+        bv[0][j] = lds_read16(ad);
+        bv[1][j] = lds_read16(ad ^ 64u);
       }
+    }
+    // A fragments (k halves 0 and 1: slot ^ 4 = LDS address ^ 64)
+    u32x4_t av[2][MI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      av[0][i] = lds_read16(wbase + aoff[i]);
+      av[1][i] = lds_read16((wbase + aoff[i]) ^ 64u);
+    }
+    // next step's B fragments, in flight during this step's MFMAs
+    const bool pre = tap + 1 < RS;
+    u32x4_t bn[2][MJ];
+    if (pre) {
+      const int ds1 = ds + 1 == S ? 0 : ds + 1, dr1 = ds + 1 == S ? dr + 1 : dr;
+      const int toff = dr1 * g.hw + ds1;
+#pragma unroll
+      for (int j = 0; j < MJ; ++j) {
+        const int hp = hb0[j] + toff;
+        const uint32_t ad = hbase + (uint32_t)(hp << 7) + (uint32_t)((fk ^ halo_swz(hp)) << 4);
+        bn[0][j] = lds_read16(ad);
+        bn[1][j] = lds_read16(ad ^ 64u);
+      }
+      static_assert(2 * MJ <= 15, "lgkmcnt range");
+      asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(2 * MJ) : "memory");  // this step's A and B landed
+    } else {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < MJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, av[kh][i]),
+                                                              __builtin_bit_cast(bf16x8_t, bv[kh][j]), acc[i][j], 0, 0,
+                                                              0);
+    if (pre) {
+#pragma unroll
+      for (int j = 0; j < MJ; ++j) {
+        bv[0][j] = bn[0][j];
+        bv[1][j] = bn[1][j];
+      }
+    }
+    // advance the compute step (incremental: no scalar divisions in the loop)
+    cslot = cslot + 1 == NWB ? 0 : cslot + 1;
+    if (++ds == S) {
+      ds = 0;
+      ++dr;
+    }
+    if (++tap == RS) {
+      tap = dr = ds = 0;
+      ++chunk;
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // every fragment read done before the epilogue reuses the LDS
+  const EpiRowHalo rmap{g.fpr, a.Q, g.th, M};
   constexpr int NH = (BP * BC * 4 > 160 * 1024) ? 2 : 1;
   if constexpr (NH == 1) {
-    EpiPre<BP, BC, NT, false> epre;
-    epi_prefetch<BP, BC, NT, false>(a, m0, c0, m_end, epre);
-    conv_epilogue<BP, BC, WP, WC, MI, MJ, NT, false>(a, smem, acc, wp, wc, m0, c0, m_end, epre);
+    EpiPre<BP, BC, NT, false> epre;  // (unused: lazy per-row offsets through the row map)
+    conv_epilogue_pass<BP, BC, WP, MI, MJ, NT, false, true, EpiRowHalo>(a, smem, acc, true, wp, wc * WC, m0, c0, M,
+                                                                        epre, rmap);
   } else {
-    conv_epilogue_sliced<BP, BC, WP, WC, MI, MJ, NT, NH>(a, smem, acc, wp, wc, m0, c0, m_end);
+    conv_epilogue_sliced<BP, BC, WP, WC, MI, MJ, NT, NH, EpiRowHalo>(a, smem, acc, wp, wc, m0, c0, M, rmap);
   }
 }
 
@@ -249,47 +367,40 @@ __global__ __launch_bounds__(512) void conv_halo_kernel(DrnConvFwdArgs a, HaloGe
 //   0: 224 px x 128 ch (28x28 / 14x14 / 7x7 stages), 3 steps in flight
 //   1: 256 px x 64 ch (56x56, 64 channels), 3 in flight
 //   2: 448 px x 64 ch (56x56, 8 rows per tile)
-//   3: 224 px x 256 ch, 2 in flight (LDS)
+//   3: 256 px x 128 ch, 4 x 4 fragments per wave (32 FLOP per LDS byte), 2 in flight
 //   4: 128 px x 128 ch (7x7: 2 images per tile)
 //   5: 256 px x 64 ch, every wave all 64 channels of 32 pixels
 #define DRN_HALO_CONFIGS(X) \
   X(0, 2, 7, 4, 2, 3)       \
   X(1, 4, 4, 2, 2, 3)       \
   X(2, 4, 7, 2, 2, 3)       \
-  X(3, 2, 7, 4, 4, 2)       \
+  X(3, 4, 4, 2, 4, 2)       \
   X(4, 2, 4, 4, 2, 3)       \
   X(5, 8, 2, 1, 4, 3)
 #define DRN_HALO_NCFG 6
-#define DRN_HALO_HPW 12
+#define DRN_HALO_HPW 8
 
-// tile geometry for a computed pixel width BP: the largest tile of whole output rows (th | P) or
-// whole images that fits BP; 0 if none
+// tile geometry for a computed pixel width BP: the most output rows th (th | P) whose fragments
+// (fpr per row) fit BP; 0 if not even one row fits
 static int halo_geom(const DrnConvFwdArgs* a, int BP, HaloGeom* g) {
   const int P = a->P, Q = a->Q;
-  g->ni = 1;
+  g->fpr = (Q + 15) / 16;
   g->th = 0;
-  if (P * Q <= BP) {
-    g->th = P;
-    g->ni = BP / (P * Q);
-    if (g->ni > a->N) g->ni = a->N;
-  } else {
-    for (int th = P; th >= 1; --th)
-      if (P % th == 0 && th * Q <= BP) {
-        g->th = th;
-        break;
-      }
-  }
+  for (int th = P; th >= 1; --th)
+    if (P % th == 0 && th * g->fpr * 16 <= BP) {
+      g->th = th;
+      break;
+    }
   if (g->th == 0) return 0;
   g->tpi = P / g->th;
   g->hh = g->th + a->R - 1;
   g->hw = Q + a->S - 1;
-  g->hpx = g->ni * g->hh * g->hw;
-  g->tp = g->ni * g->th * Q;
-  g->ntp = g->ni > 1 ? (a->N + g->ni - 1) / g->ni : a->N * g->tpi;
+  g->hpx = g->hh * g->hw;
+  g->ntp = a->N * g->tpi;
   return 1;
 }
 
-template <int WAVES_P, int MJ, int WAVES_C, int MI, int D>
+template <int WAVES_P, int MJ, int WAVES_C, int MI, int D, bool PRO>
 static int launch_halo(const DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
   constexpr int BP = WAVES_P * MJ * 16, BC = WAVES_C * MI * 16;
   if (a->K % BC || a->R * a->S < D) return (int)hipErrorInvalidValue;
@@ -297,16 +408,21 @@ static int launch_halo(const DrnConvFwdArgs* a, const void* zero, hipStream_t s)
   if (!halo_geom(a, BP, &g)) return (int)hipErrorInvalidValue;
   const int npieces = (g.hpx + 7) / 8;
   if ((npieces + 7) / 8 > DRN_HALO_HPW) return (int)hipErrorInvalidValue;
+  // the spare halo KB must cover the garbage columns' reach past the halo (fpr*16 - Q + S - 1 px)
+  if (g.fpr * 16 - a->Q + a->S - 1 > 16) return (int)hipErrorInvalidValue;
   const int nchunk = a->C / 64;
-  const int hbytes = npieces * 1024;
-  const int lds_main = (nchunk > 1 ? 2 : 1) * hbytes + (D + 1) * BC * 128;
+  const int hbytes = (npieces + 2) * 1024;
+  const int lds_main = (nchunk > 1 ? 2 : 1) * hbytes + (D + 1) * BC * 128 + (PRO ? 8 * a->C : 0);
   constexpr int NH = (BP * BC * 4 > 160 * 1024) ? 2 : 1;
   const int lds_epi = BP * BC * 4 / NH;
   const int lds = lds_main > lds_epi ? lds_main : lds_epi;
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   // the runtime vmcnt switch covers counts up to 30
   if ((D - 1) * (BC / 64) + (npieces + 7) / 8 > 30) return (int)hipErrorInvalidValue;
-  auto kern = conv_halo_kernel<WAVES_P, MJ, WAVES_C, MI, D, DRN_HALO_HPW>;
+  if (PRO && a->in_fin.stats != nullptr &&
+      (a->in_fin.C != a->C || a->in_fin.G < 1 || a->in_fin.G > DRN_BN_FIN_GMAX))
+    return (int)hipErrorInvalidValue;
+  auto kern = conv_halo_kernel<WAVES_P, MJ, WAVES_C, MI, D, DRN_HALO_HPW, PRO>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -321,10 +437,12 @@ static int launch_halo(const DrnConvFwdArgs* a, const void* zero, hipStream_t s)
 }  // namespace drn
 
 // Whether the halo kernel family supports this convolution (stride 1, R, S <= 3 with SAME
-// padding, 64-channel chunks, identity output map, plain input: no fused BN prologue).
+// padding, 64-channel chunks, identity output map; a fused BN-apply + ReLU input prologue is
+// supported, the BN-backward input transform is not).
 DRN_API int drn_conv_halo_ok(const DrnConvFwdArgs* a) {
   return a->stride == 1 && a->dil == 1 && a->R <= 3 && a->S <= 3 && a->R >= 1 && a->S >= 1 && a->C % 64 == 0 &&
-         a->K % 64 == 0 && a->in_scale == nullptr && a->bnb_x == nullptr && a->out_stride == 0 && a->ksplit <= 1 &&
+         a->C <= 4096 && a->K % 64 == 0 && (a->in_scale == nullptr || a->relu_in != 0) && a->bnb_x == nullptr &&
+         a->out_stride == 0 && a->ksplit <= 1 &&
          a->sk_blocks == 0 && a->fin_cnt == nullptr && a->P == a->H && a->Q == a->W && a->pad_h >= 0 &&
          a->pad_w >= 0 && a->pad_h < a->R && a->pad_w < a->S;
 }
@@ -334,9 +452,10 @@ DRN_API int drn_conv_halo_num_cfgs() { return DRN_HALO_NCFG; }
 DRN_API int drn_conv_halo(int cfg, const DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
   if (!drn_conv_halo_ok(a) || zero == nullptr) return (int)hipErrorInvalidValue;
   switch (cfg) {
-#define DRN_X(id, wp, mj, wc, mi, d) \
-  case id:                           \
-    return drn::launch_halo<wp, mj, wc, mi, d>(a, zero, s);
+#define DRN_X(id, wp, mj, wc, mi, d)                                                      \
+  case id:                                                                                \
+    return a->in_scale != nullptr ? drn::launch_halo<wp, mj, wc, mi, d, true>(a, zero, s) \
+                                  : drn::launch_halo<wp, mj, wc, mi, d, false>(a, zero, s);
     DRN_HALO_CONFIGS(DRN_X)
 #undef DRN_X
     default:

@@ -162,13 +162,17 @@ class Executor:
         # per consuming tile, and the streaming pass it replaces is pure HBM traffic -- and
         # materialise BNs feeding a 3x3 conv, whose 9 taps would transform every element 9 times.
         # "all" materialises every BN, "none" fuses every BN (DRN_BN_MATERIALIZE).
+        # "halo": as "1x1", but BNs feeding a stride-1 3x3 conv are fused too (the halo-tiled
+        # kernel, conv_halo.hip, transforms each staged input element once per tile instead of
+        # once per tap). Measured slower than materialising (ResNet-50 bs128, one box, 2 rounds:
+        # 12,926-12,930 vs 13,097-13,102 img/s, profiles/r4_experiments.md): kept as an option.
         if materialize_bn is None:
             policy = os.environ.get("DRN_BN_MATERIALIZE", "1x1" if self.is_hip else "all")
             if os.environ.get("DRN_FUSE_BN_PROLOGUE") == "1":
                 policy = "none"
         else:
             policy = "all" if materialize_bn else "none"
-        assert policy in ("all", "1x1", "none"), policy
+        assert policy in ("all", "1x1", "halo", "none"), policy
         self.bn_policy = policy
         self.materialize_bn = policy != "none"
         # ... and (policy "1x1") BNs whose 1x1 consumer has >= DRN_BN_MAT_TILES 128-wide output-
@@ -409,9 +413,12 @@ class Executor:
             for i, b in enumerate(bp.bn):
                 consumers = [bp.convs[i].conv] + ([bp.proj.conv] if i == 0 and bp.proj is not None else [])
                 big = b.src.numel() >= self.mat_min_elems
-                if self.bn_policy == "all" or (self.bn_policy == "1x1" and big and (
-                        any(c.k != 1 for c in consumers) or
-                        max(-(-c.cout // 128) for c in consumers) >= self.mat_tiles)):
+
+                def fusable(c):
+                    halo = self.bn_policy == "halo" and c.k == 3 and c.stride == 1 and c.cin_store % 64 == 0
+                    return (c.k == 1 or halo) and -(-c.cout // 128) < self.mat_tiles
+                if self.bn_policy == "all" or (self.bn_policy in ("1x1", "halo") and big and
+                                               not all(fusable(c) for c in consumers)):
                     b.act = self._act(*b.src.shape)
         for b in [b for bp in self.blocks for b in bp.bn] + [self.final_bn]:
             b.bacc, b.bG = self._stats_for(b.rows, b.bn.c)
@@ -437,17 +444,16 @@ class Executor:
         # (profiles/r3s2_gradbufs.txt). Default 32 (~6.5 GB at ResNet-50 bs128), at most ~8 % of
         # the device memory, for ImageNet-sized activations; small ones (CIFAR: latency-bound
         # kernels on L2-resident tensors, 2.06-2.28 ms with 32 buffers vs 1.8-2.1 ms) keep 6.
-        # Multi-rank data parallelism keeps 6: the bucket all-reduces are issued from the side
-        # stream once it has caught up (_report), so a side stream running further behind would
-        # start them later and expose more communication after the backward pass (unmeasured at
-        # N > 1: no multi-GPU box here).
+        # Data parallelism uses the same pool: a bucket's all-reduce is issued from the side
+        # stream right after the bucket's last weight gradient (_report), which is the earliest
+        # point its data exists whatever the pool size; the pool only decides how long the
+        # critical-path data gradients wait for side-stream readers (single-rank RCCL engine,
+        # ResNet-50 bs128: 10.02 ms vs 9.87 ms plain, profiles/r4_base).
         nbuf_env = os.environ.get("DRN_GRAD_BUFS")
         buf_bytes = max_act * torch.finfo(self.be.act_dtype).bits // 8
-        import torch.distributed as _dist
-        multi_rank = _dist.is_available() and _dist.is_initialized() and _dist.get_world_size() > 1
         if nbuf_env is not None:
             nbuf = max(3, int(nbuf_env))
-        elif self.side is not None and buf_bytes >= (64 << 20) and not multi_rank:
+        elif self.side is not None and buf_bytes >= (64 << 20):
             cap = int(0.08 * torch.cuda.get_device_properties(self.device).total_memory) // max(1, buf_bytes) \
                 if self.device.type == "cuda" else 32
             nbuf = max(6, min(32, cap))
