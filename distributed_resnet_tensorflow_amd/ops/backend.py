@@ -248,6 +248,11 @@ class HipBackend(_Common):
         self.tune_log: list = []
         self._db = None   # persistent kernel-selection database (ops/tunedb.py), loaded on first use
         self.db_hits = 0
+        # tuner effort: first-pass launches per candidate, finalists re-timed, re-timing rounds
+        # (scripts/make_tune_db.py raises them when it builds the shipped database)
+        self.tune_iters = int(os.environ.get("DRN_TUNE_ITERS", "5"))
+        self.tune_top = int(os.environ.get("DRN_TUNE_TOP", "4"))
+        self.tune_rounds = int(os.environ.get("DRN_TUNE_ROUNDS", "2"))
 
     def tune_db(self):
         if self._db is None:
@@ -372,7 +377,7 @@ class HipBackend(_Common):
             self._set_ksplit(a, ks)
         _lib.check(self.L.drn_conv_fwd2(ctypes.byref(a), self.zero_page.data_ptr(), self.stream()), "drn_conv_fwd")
 
-    def _tune_conv(self, a, key, iters: int = 5) -> int:
+    def _tune_conv(self, a, key, iters: int = 0) -> int:
         """Time every kernel configuration for this geometry (the MIOpen 'find' step, done once
         per distinct convolution before the step is captured) and return the fastest. Runs on
         scratch outputs / statistics so no live buffer is modified. Every configuration
@@ -380,6 +385,7 @@ class HipBackend(_Common):
         halo = bool(self.L.drn_conv_halo_ok(ctypes.byref(a)))
         if not self.L.drn_conv_glds_ok(ctypes.byref(a)) and not halo:
             return (100, 1)
+        iters = iters or self.tune_iters
         N, K = a.N, a.K
         oh = a.out_H if a.out_stride else a.P
         ow = a.out_W if a.out_stride else a.Q
@@ -444,8 +450,8 @@ class HipBackend(_Common):
                 continue  # configuration not applicable to this geometry (e.g. C % 64 != 0)
             first.append((time_cfg(c, iters), c))
         first.sort()
-        top = {c: ms for ms, c in first[:4 if os.environ.get("DRN_TUNE_2PASS", "1") == "1" else 1]}
-        for _ in range(2 if len(top) > 1 else 0):
+        top = {c: ms for ms, c in first[:self.tune_top if os.environ.get("DRN_TUNE_2PASS", "1") == "1" else 1]}
+        for _ in range(self.tune_rounds if len(top) > 1 else 0):
             for c in list(top):
                 top[c] = min(top[c], time_cfg(c, 2 * iters))
         best, best_t = min(top.items(), key=lambda kv: kv[1]) if top else ((100, 1), 0.0)
@@ -552,11 +558,12 @@ class HipBackend(_Common):
             _lib.check(self.L.drn_splitk_reduce(a.out, out.data_ptr(), out.numel(), a.splits, 1.0, 0, st),
                        "drn_splitk_reduce")
 
-    def _tune_wgrad(self, args_for, out, key, iters: int = 5) -> tuple:
+    def _tune_wgrad(self, args_for, out, key, iters: int = 0) -> tuple:
         """Pick (split-K target, pipeline) by timing the weight-gradient kernel TOGETHER with its
         split-K reduction: 0 = register-staged, 2/3 = LDS-DMA stages of 64 pixels, 4/5/6 = 2/3/4
         stages of 32 pixels. Writes only the workspace and this gradient slot (rewritten by the
         real launch that follows)."""
+        iters = iters or self.tune_iters
         st = self.stream()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         cands = tuple(int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6,7,8").split(","))
@@ -590,8 +597,8 @@ class HipBackend(_Common):
         # best -- single 5-launch timings of ~10-us CIFAR kernels picked outliers (run-to-run step
         # spread 1.77-1.95 ms at batch 32)
         first.sort(key=lambda r: r[0])
-        top = [[ms, cfg, a] for ms, cfg, a in first[:4]]
-        for _ in range(2 if len(top) > 1 else 0):
+        top = [[ms, cfg, a] for ms, cfg, a in first[:self.tune_top]]
+        for _ in range(self.tune_rounds if len(top) > 1 else 0):
             for r in top:
                 r[0] = min(r[0], time_one(r[2], r[1][1], 2 * iters))
         best_t, best, _ = min(top, key=lambda r: r[0])
