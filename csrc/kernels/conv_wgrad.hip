@@ -50,10 +50,14 @@ static bool getenv_flag(const char* name, bool dflt) {
   return e == nullptr ? dflt : atoi(e) != 0;
 }
 
-// 32-byte-slot swizzle for rows of W bytes (W = 128 or 256)
+// 32-byte-slot swizzle for rows of W bytes (W = 64, 128 or 256). W = 64 (the narrow 32-channel
+// dY image of the K <= 32 weight gradients): 2 slots per row; the transposed fragment reads of
+// one 32-lane half touch rows {r..r+3, r+8..r+11} at 4 byte offsets each, rows r and r+8 share
+// their banks (4 rows per 256-byte bank row), so bit 3 of the row flips the slot.
 template <int W>
 __device__ __forceinline__ int slot_swz(int row) {
   if constexpr (W == 256) return (row & 3) | (((row >> 3) & 1) << 2);
+  if constexpr (W == 64) return (row >> 3) & 1;
   return ((row >> 1) & 1) | (((row >> 3) & 1) << 1);
 }
 
@@ -857,8 +861,21 @@ static int launch_wgrad_glds_p(DrnConvWgradArgs* a, const void* zero, hipStream_
   return (int)hipGetLastError();
 }
 
+template <int BKK, int BCO, int NS, int BP, bool IL>
+static int launch_wgrad_glds_ok(DrnConvWgradArgs* a, const void* zero, hipStream_t s);
+
 template <int BKK, int BCO, int NS, int BP = 64, bool IL = false>
 static int launch_wgrad_glds(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
+  // (every wave issues >= 1 dY LDS-DMA instruction per stage: BP rows of 2*BCO bytes)
+  if constexpr (BP * BCO * 2 < 4 * 1024) {
+    return (int)hipErrorInvalidValue;
+  } else {
+    return launch_wgrad_glds_ok<BKK, BCO, NS, BP, IL>(a, zero, s);
+  }
+}
+
+template <int BKK, int BCO, int NS, int BP, bool IL>
+static int launch_wgrad_glds_ok(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
 #ifndef DRN_NO_FAST_LOADER
   static const bool lin_on = getenv_flag("DRN_WGRAD_LIN", true);
 #else
@@ -889,6 +906,14 @@ static int dispatch_wgrad_tile(DrnConvWgradArgs* a, const void* zero, hipStream_
   const int Ktot = a->R * a->S * a->C;
   const bool wide_k = Ktot > 64;
   const bool wide_c = a->K > 64;
+  if (a->K <= 32) {
+    // narrow output (CIFAR stages 1-2: 16 / 32 filters, reference resnet_model_official.py:
+    // 255-266): 32-channel dY tiles (a 64-wide tile wasted 50-75 % of the MFMA work) and the
+    // k tile that pads R*S*C least (144 -> 192 instead of 256, 288 -> 320 instead of 384)
+    const bool k128 = wide_k && ((Ktot + 127) / 128) * 128 <= ((Ktot + 63) / 64) * 64;
+    if (k128) return launch_wgrad_glds<128, 32, NS, BP, IL>(a, zero, s);
+    return launch_wgrad_glds<64, 32, NS, BP, IL>(a, zero, s);
+  }
   if (wide_k && wide_c) return launch_wgrad_glds<128, 128, NS, BP, IL>(a, zero, s);
   if (wide_k) return launch_wgrad_glds<128, 64, NS, BP, IL>(a, zero, s);
   if (wide_c) return launch_wgrad_glds<64, 128, NS, BP, IL>(a, zero, s);
@@ -980,7 +1005,11 @@ DRN_API int drn_wgrad_trace_set(unsigned long long* buf) {
 
 // Block-tile shape the dispatcher picks (host mirror used to size the split-K grid).
 DRN_API int drn_wgrad_tiles(int Ktot, int K) {
-  const int bkk = Ktot > 64 ? 128 : 64, bco = K > 64 ? 128 : 64;
+  int bkk = Ktot > 64 ? 128 : 64, bco = K > 64 ? 128 : 64;
+  if (K <= 32) {  // (dispatch_wgrad_tile's narrow-output tiles)
+    bco = 32;
+    bkk = (Ktot > 64 && ((Ktot + 127) / 128) * 128 <= ((Ktot + 63) / 64) * 64) ? 128 : 64;
+  }
   return ((Ktot + bkk - 1) / bkk) * ((K + bco - 1) / bco);
 }
 

@@ -483,6 +483,9 @@ class HipBackend(_Common):
         min_steps = min_steps or HipBackend.WGRAD_MIN_STEPS
         bkk = 128 if Ktot > 64 else 64
         bco = 128 if K > 64 else 64
+        if K <= 32:  # the narrow-output tiles of csrc/kernels/conv_wgrad.hip dispatch_wgrad_tile
+            bco = 32
+            bkk = 128 if (Ktot > 64 and -(-Ktot // 128) * 128 <= -(-Ktot // 64) * 64) else 64
         tiles = ((Ktot + bkk - 1) // bkk) * ((K + bco - 1) // bco)
         steps = (M + 63) // 64
         # never MORE blocks than the target (rounding the split count up made e.g. 36 tiles x 15

@@ -151,6 +151,8 @@ class Executor:
         # (Forking the projection-shortcut forward conv onto this stream measured neutral, and a
         # CU-masked side stream +0-0.4 %; both were removed.)
         self.side = None
+        # the data-gradient weight refresh after each update on the side stream (eager steps)
+        self.tflip_side = os.environ.get("DRN_TFLIP_SIDE", "1") == "1"
         if self.is_hip and os.environ.get("DRN_WGRAD_STREAM", "1") == "1":
             self.side = torch.cuda.Stream(self.device)
         self._pending = {}
@@ -318,6 +320,8 @@ class Executor:
         if mode == "0" or (mode == "auto" and stem_macs < 1e9):
             self._stem_hi = 0
         self._tail_ev = None
+        self._stem_ev = None   # side stream: the stem's weight gradient (issued last) is done
+        self._tflip_ev = None  # side stream: the data-gradient weights of the next backward are ready
         img = sp.image_size
         self.images = self._act(N, img, img, sp.stem.cin_store)
         # Packed stem (csrc/kernels/stem.hip, DRN_STEM_PACK=1 default on HIP): the 7x7/2 stem over
@@ -666,6 +670,12 @@ class Executor:
         self._report(self.P.by_name[f"{fb.bn.name}/gamma"].offset)
         cur = self._lru[-1]  # index of the buffer holding d_out
         self._pending.clear()
+        if self._tflip_ev is not None:  # the flipped weights refreshed on the side stream
+            # (a capture starts after its eager warm-up has synchronized: the event is complete,
+            # and a graph may not wait on an event recorded outside it)
+            if not (self.is_hip and torch.cuda.is_current_stream_capturing()):
+                torch.cuda.current_stream(self.device).wait_event(self._tflip_ev)
+            self._tflip_ev = None
         for bp in reversed(self.blocks):
             cur = self._block_bwd(bp, bufs, cur)
             if self.check_nan:
@@ -696,6 +706,9 @@ class Executor:
                         post=lambda: be.stem_unpack_grad(self.stem_dw4, st.dw))
         else:
             self._wgrad(self.images, d_stem, st.dw, st.geom)
+        if self._tail_ev is not None:
+            self._stem_ev = torch.cuda.Event()
+            self._stem_ev.record(self.side)
         self._report(0)
         if self._tail_ev is None:
             self._join()
@@ -837,10 +850,13 @@ class Executor:
         self.be.fill_(self.lr_t, float(lr))
 
     def join_grads(self):
-        """Make the current stream wait for a stem weight gradient deferred by backward()."""
+        """Make the current stream wait for a stem weight gradient deferred by backward() (its
+        event only: work queued on the side stream after it -- the data-gradient weight refresh
+        -- is not waited for)."""
         if self._tail_ev is not None:
             self._tail_ev = None
-            self._join()
+            ev, self._stem_ev = self._stem_ev, None
+            self._join(ev)
 
     def apply_gradients(self, grad_scale: float = 1.0, grad: Optional[torch.Tensor] = None,
                         skip: Optional[torch.Tensor] = None):
@@ -877,12 +893,23 @@ class Executor:
 
     def refresh_dgrad_weights(self, stem: bool = True):
         """Rebuild the flipped / channel-transposed data-gradient weights (and the packed stem's
-        weights) from the compute copy."""
+        weights) from the compute copy. Eager steps with the side stream run the rebuild there:
+        only the NEXT backward's data gradients read these weights, so it overlaps the next
+        forward pass instead of sitting between the update and the next step (the backward waits
+        for its event). A captured step keeps it on the capturing stream (a graph must rejoin
+        every forked stream before it ends)."""
         P = self.P
         if self.wt_n:
             src = P.wbf16 if P.wbf16 is not None else P.master
             table = self.wt_table if self.is_hip else self.wt_table.cpu()
-            self.be.weight_tflip(src, self.wt_flat, table, self.wt_n, self.wt_total)
+            if self.side is not None and self.tflip_side and not torch.cuda.is_current_stream_capturing():
+                self.side.wait_stream(torch.cuda.current_stream(self.device))  # the updated weights
+                with torch.cuda.stream(self.side):
+                    self.be.weight_tflip(src, self.wt_flat, table, self.wt_n, self.wt_total)
+                self._tflip_ev = torch.cuda.Event()
+                self._tflip_ev.record(self.side)
+            else:
+                self.be.weight_tflip(src, self.wt_flat, table, self.wt_n, self.wt_total)
         if stem:
             self._repack_stem()
 
