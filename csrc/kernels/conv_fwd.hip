@@ -1086,6 +1086,18 @@ static int cfin_max_blocks() {
   return v;
 }
 
+// ... and a grid whose workgroups would each re-derive many channels: the prologue finalize
+// reads G replicas x C channels per workgroup from L2 (ResNet-50 stage 4: 392 workgroups x 2048
+// channels x 64 B = 51 MB, 8 dependent channel rounds per thread)
+static long cfin_max_work() {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("DRN_CFIN_MAX_WORK");
+    v = e ? atol(e) : (1L << 19);
+  }
+  return v;
+}
+
 template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF, int BK, bool PRO, bool SROW = false, bool BNB = false,
           int NH = 1, bool KS = false, bool IL = false>
 static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
@@ -1123,7 +1135,8 @@ static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t 
   }
   const int ks = KS ? a->ksplit : 1;
   if (KS && (ks < 2 || T < ks || a->ks_ws == nullptr || a->ks_tickets == nullptr)) return (int)hipErrorInvalidValue;
-  if (PRO && a->in_fin.stats != nullptr && tiles_p * tiles_c * ks > cfin_max_blocks()) {
+  if (PRO && a->in_fin.stats != nullptr &&
+      (tiles_p * tiles_c * ks > cfin_max_blocks() || (long)a->C * tiles_p * tiles_c * ks > cfin_max_work())) {
     // a large grid pays the in-prologue finalize once per workgroup wave: measured slower than
     // one separate finalize launch (ResNet-50 stage 1, 12544 workgroups: +11 us vs ~6 us)
     if (a->in_fin.publish) {

@@ -253,11 +253,40 @@ class HipBackend(_Common):
         self.tune_iters = int(os.environ.get("DRN_TUNE_ITERS", "5"))
         self.tune_top = int(os.environ.get("DRN_TUNE_TOP", "4"))
         self.tune_rounds = int(os.environ.get("DRN_TUNE_ROUNDS", "2"))
+        # cold timing: every timed launch follows a 64 MB scratch write that evicts the L2s (the
+        # operands stay in the Infinity Cache) -- inside a training step a conv reads what the
+        # previous kernel wrote from other XCDs, never its own L2-warm copy of a re-launched input
+        self.tune_cold = os.environ.get("DRN_TUNE_COLD", "0") == "1"
+        self._evict_buf = None
+        self._fin_bufs: dict = {}
+
+    def _timed(self, launch, n: int) -> float:
+        """Mean ms of n launches of launch() on the current stream (cold: one L2 eviction before
+        each, bracketed per launch so the eviction is not timed)."""
+        if not self.tune_cold:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+            for _ in range(n):
+                launch()
+            ev1.record()
+            ev1.synchronize()
+            return ev0.elapsed_time(ev1) / n
+        if self._evict_buf is None:
+            self._evict_buf = torch.empty(16 << 20, dtype=torch.float32, device=self.device)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+        for e0, e1 in evs:
+            self._evict_buf.zero_()
+            e0.record()
+            launch()
+            e1.record()
+        evs[-1][1].synchronize()
+        return sum(e0.elapsed_time(e1) for e0, e1 in evs) / n
 
     def tune_db(self):
         if self._db is None:
             from .tunedb import TuneDB, section_for
-            self._db = TuneDB(section_for(self.device, self.L))
+            # (cold- and warm-timed choices differ: the timing mode is part of the section)
+            self._db = TuneDB(section_for(self.device, self.L) + ("-cold" if self.tune_cold else ""))
         return self._db
 
     def save_tune_db(self) -> bool:
@@ -402,7 +431,6 @@ class HipBackend(_Common):
         t.in_fin.publish = 0
         t.bnb_fin.publish = 0
         s = self.stream()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         cands = os.environ.get("DRN_CONV_CANDS")
         if cands:
             cands = [int(c) for c in cands.split(",")]
@@ -419,13 +447,10 @@ class HipBackend(_Common):
 
         def time_cfg(c, n):
             setk(c)
-            _lib.check(self.L.drn_conv_fwd2(ctypes.byref(t), self.zero_page.data_ptr(), s), "drn_conv_fwd")
-            ev0.record()
-            for _ in range(n):
-                _lib.check(self.L.drn_conv_fwd2(ctypes.byref(t), self.zero_page.data_ptr(), s), "drn_conv_fwd")
-            ev1.record()
-            ev1.synchronize()
-            return ev0.elapsed_time(ev1) / n
+            launch = lambda: _lib.check(self.L.drn_conv_fwd2(ctypes.byref(t), self.zero_page.data_ptr(), s),  # noqa
+                                        "drn_conv_fwd")
+            launch()
+            return self._timed(launch, n)
 
         # candidates: (config, split-K factor); split-K only where the grid leaves CUs idle
         M = a.N * a.P * a.Q
@@ -568,18 +593,12 @@ class HipBackend(_Common):
         real launch that follows)."""
         iters = iters or self.tune_iters
         st = self.stream()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         cands = tuple(int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6,7,8").split(","))
         seen = set()
         modes = (False, True) if self.wgrad_atomic_ok else (False,)
 
         def time_one(a, ns, n):
-            ev0.record()
-            for _ in range(n):
-                self._wgrad_full(a, ns, out, st)
-            ev1.record()
-            ev1.synchronize()
-            return ev0.elapsed_time(ev1) / n
+            return self._timed(lambda: self._wgrad_full(a, ns, out, st), n)
 
         first = []  # (ms, (target, pipeline, atomic, min steps), args)
         for tgt, atomic, ms_min in [(t, m, k) for t in self.WGRAD_TARGETS for m in modes
@@ -697,13 +716,45 @@ class HipBackend(_Common):
 
     def bn_apply_fin(self, x, y, fin: BnCfin, relu=True):
         C = x.shape[-1]
+        if C >= self.BN_FIN_SPLIT_C and fin.publish:
+            # (the publishing consumer: one finalize launch writes scale / shift / moving
+            # averages, the plain apply reads them; a non-publishing consumer keeps the fused
+            # prologue, since nothing orders it after the publisher)
+            self.bn_finalize(fin.stats, fin.G, fin.count, fin.gamma, fin.beta, fin.run_mean, fin.run_var, fin.scale,
+                             fin.shift, fin.mean, fin.invstd, fin.momentum, fin.eps,
+                             update_running=fin.run_mean is not None)
+            self.bn_apply(x, y, fin.scale, fin.shift, relu=relu)
+            return
         f = fin.struct()
         _lib.check(self.L.drn_bn_apply_fin(x.data_ptr(), y.data_ptr(), ctypes.byref(f), x.numel() // C, C,
                                            1 if relu else 0, self.stream()), "drn_bn_apply_fin")
 
+    # consumer-side finalize costs every workgroup of the apply C channels x G replicas of L2
+    # reads in its prologue (2048 workgroups x 2048 channels x 64 B = 268 MB at the last stage of
+    # ResNet-50): from this many channels on, one small finalize launch computes the
+    # coefficients once and the apply reads only its own 8 channels'
+    BN_FIN_SPLIT_C = int(os.environ.get("DRN_BN_FIN_SPLIT_C", "512"))
+
+    def _fin_scratch(self, C: int) -> torch.Tensor:
+        """[coef 3C][dgamma C][dbeta C] fp32 scratch of the split backward finalize (one per C:
+        the BatchNorm-backward applies run in order on one stream); allocated by the eager
+        warm-up step, before any graph capture."""
+        buf = self._fin_bufs.get(C)
+        if buf is None:
+            buf = self._fin_bufs[C] = torch.empty(5 * C, dtype=torch.float32, device=self.device)
+        return buf
+
     def bn_bwd_apply_fin(self, dy, dpool, pool_hw, x, scale, shift, fin: BnCfin, add, dx, relu=True):
         C = x.shape[-1]
         _aligned16(scale, shift)
+        if C >= self.BN_FIN_SPLIT_C:
+            buf = self._fin_scratch(C)
+            coef = buf[:3 * C]
+            dg = fin.dgamma if fin.publish else buf[3 * C:4 * C]
+            db = fin.dbeta if fin.publish else buf[4 * C:]
+            self.bn_finalize_bwd(fin.stats, fin.G, fin.count, fin.gamma, fin.invstd, dg, db, coef)
+            self.bn_bwd_apply(dy, dpool, pool_hw, x, scale, shift, fin.mean, fin.invstd, coef, add, dx, relu=relu)
+            return
         f = fin.struct()
         _lib.check(self.L.drn_bn_bwd_apply_fin(_ptr(dy), _ptr(dpool), pool_hw, x.data_ptr(), scale.data_ptr(),
                                                shift.data_ptr(), ctypes.byref(f), _ptr(add), dx.data_ptr(),

@@ -153,6 +153,8 @@ class Executor:
         self.side = None
         # the data-gradient weight refresh after each update on the side stream (eager steps)
         self.tflip_side = os.environ.get("DRN_TFLIP_SIDE", "1") == "1"
+        # gradient-buffer claims skip the cross-queue wait when the reader already finished
+        self.claim_query = os.environ.get("DRN_CLAIM_QUERY", "1") == "1"
         if self.is_hip and os.environ.get("DRN_WGRAD_STREAM", "1") == "1":
             self.side = torch.cuda.Stream(self.device)
         self._pending = {}
@@ -751,8 +753,14 @@ class Executor:
         """Before the main stream writes a rotating gradient buffer: wait for the side-stream
         weight gradient still reading it."""
         ev = self._pending.pop(id(buf), None)
-        if ev is not None:
-            torch.cuda.current_stream(self.device).wait_event(ev)
+        if ev is None:
+            return
+        # an event that has already completed needs no cross-queue barrier packet (each one
+        # costs the main queue a few us before the next kernel starts); inside a capture the
+        # dependency must be recorded as a graph edge regardless
+        if self.claim_query and not torch.cuda.is_current_stream_capturing() and ev.query():
+            return
+        torch.cuda.current_stream(self.device).wait_event(ev)
 
     def _join(self, ev=None):
         if self.side is None:

@@ -80,6 +80,12 @@ class SegmentedStepGraph:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
 
+    @property
+    def side_stream(self):
+        """The executor's weight-gradient side stream this graph took off it (an eager step
+        that replaces the graph puts it back)."""
+        return self._side
+
     def _reduced_grad(self):
         return self.eng.wire_buf if self.eng.wire_buf is not None else self.ex.P.grad
 

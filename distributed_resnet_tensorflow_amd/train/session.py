@@ -88,12 +88,20 @@ class TrainingSession:
             self.ex.autotune()  # fix kernel configurations before any collective / graph capture
         # one GPU: the whole step is one HIP graph. Data parallel with the P2P all-reduce (every
         # collective is a kernel with device-side flags): also the whole step, comm included, in
-        # one graph. Data parallel over RCCL: eager (measured faster than the chain
-        # of per-segment graphs, SegmentedStepGraph, which DRN_DP_GRAPH=1 selects)
+        # one graph. Data parallel over RCCL: the chain of per-segment graphs
+        # (SegmentedStepGraph) or eager, whichever the first steps measure faster
+        # (DRN_DP_GRAPH=auto, the default; 1 / 0 force one): ImageNet ResNet-50 runs faster
+        # eager (side-stream weight gradients), CIFAR steps are launch-bound eager (~260 Python
+        # launches for a ~2 ms step) and run faster as graphs
         dp_ok = dp and self.engine.mode == "sync" and not self.sharded
-        self.use_graph = use_graph and self.device.type == "cuda" and self.be.name == "hip" and (
-            not dp or (dp_ok and self.engine.p2p is not None) or
-            (dp_ok and os.environ.get("DRN_DP_GRAPH") == "1"))
+        dp_graph = os.environ.get("DRN_DP_GRAPH", "auto")
+        hip_cuda = self.device.type == "cuda" and self.be.name == "hip"
+        self.use_graph = use_graph and hip_cuda and (
+            not dp or (dp_ok and self.engine.p2p is not None) or (dp_ok and dp_graph == "1"))
+        # eager-vs-segmented-graph trial: [phase, steps in phase, t0, eager ms/step]
+        self._trial = ["eager", 0, 0.0, 0.0] if (use_graph and hip_cuda and dp_ok and self.engine.p2p is None
+                                                and dp_graph == "auto") else None
+        self.graph_choice: Optional[dict] = None
         if not self.use_graph and self.device.type == "cuda" and self.be.name == "hip":
             # eager step (data parallel or not): the critical path on its own high-priority HW
             # queue, ahead of the weight-gradient side stream (ResNet-50 bs128 on one GPU: 9.93 vs
@@ -179,6 +187,8 @@ class TrainingSession:
                     self._graph.replay()
                 if self.engine is not None:
                     self.engine.replay_end()
+        elif self._trial is not None and not self.ex.check_nan:
+            self._trial_step()
         else:
             self._step_body()
         self.lr.after_step(self.ex.P.global_step)
@@ -186,6 +196,54 @@ class TrainingSession:
         self._metrics_cache = None
         if self.engine is not None:
             self._guard(self.engine.poll_errors)
+
+    TRIAL_WARM, TRIAL_STEPS = 3, 6
+
+    def _trial_step(self):
+        """One REAL training step of the eager-vs-segmented-graph trial (data parallel over
+        RCCL): TRIAL_WARM + TRIAL_STEPS eager steps, then the graph is built (its construction
+        runs this step eagerly and captures it), TRIAL_WARM + TRIAL_STEPS replays; the faster
+        mode stays. Both modes launch the same kernels in the same order on the same buffers:
+        the choice changes the step time, not the numerics."""
+        tr = self._trial
+        ph, n = tr[0], tr[1]
+        W, K = self.TRIAL_WARM, self.TRIAL_STEPS
+        if ph == "eager":
+            if n == W:
+                torch.cuda.synchronize(self.device)
+                tr[2] = time.perf_counter()
+            self._step_body()
+            if n == W + K - 1:
+                torch.cuda.synchronize(self.device)
+                tr[3] = (time.perf_counter() - tr[2]) / K * 1e3
+                tr[0], tr[1] = "graph", -1
+                return
+        else:
+            if self._graph is None:
+                self._graph = SegmentedStepGraph(self.ex, self.engine, 1.0 / self.world, warmup=1)
+            else:
+                if n == W:
+                    torch.cuda.synchronize(self.device)
+                    tr[2] = time.perf_counter()
+                self.engine.replay_begin()
+                self._graph.replay()
+                self.engine.replay_end()
+                if n == W + K - 1:
+                    torch.cuda.synchronize(self.device)
+                    graph_ms = (time.perf_counter() - tr[2]) / K * 1e3
+                    keep = graph_ms < tr[3]
+                    self.graph_choice = {"eager_ms": round(tr[3], 3), "graph_ms": round(graph_ms, 3),
+                                         "mode": "segmented graphs" if keep else "eager"}
+                    log.info("data-parallel step: eager %.3f ms, segmented graphs %.3f ms -> %s", tr[3], graph_ms,
+                             self.graph_choice["mode"])
+                    if keep:
+                        self.use_graph = True
+                    else:  # back to eager: drop the graphs, weight gradients back on the side stream
+                        self.ex.side = self._graph.side_stream
+                        self._graph = None
+                    self._trial = None
+                    return
+        tr[1] = n + 1
 
     def _guard(self, fn):
         """Run an error check; on failure mark the session failed (no checkpoint after it)."""

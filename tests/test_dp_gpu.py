@@ -319,3 +319,46 @@ def test_rccl_engine_bucket_schedule_matches_gloo():
     # same numbers up to the two processes' independent (timing-based) kernel autotuning and the
     # fp32-atomic accumulation order: two steps apart by ~1e-3 relative (seen up to 2.2e-3)
     assert abs(gn_n - gn_g) <= 1e-2 * max(gn_g, 1e-6)
+
+
+def _trial_worker(port, q, mode):
+    os.environ.update(DRN_FORCE_DP="1", DRN_FORCE_DP_PORT=str(port), DRN_DP_GRAPH=mode)
+    try:
+        from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2
+        from distributed_resnet_tensorflow_amd.parallel.cluster import ClusterInfo
+        from distributed_resnet_tensorflow_amd.train import lr as lr_mod
+        from distributed_resnet_tensorflow_amd.train.feeder import SyntheticFeeder
+        from distributed_resnet_tensorflow_amd.train.hooks import StopAtStepHook
+        from distributed_resnet_tensorflow_amd.train.session import TrainingSession
+        torch.cuda.set_device(0)
+        sess = TrainingSession(cifar_resnet_v2(8), 32, ClusterInfo(device="cuda:0"), weight_decay=2e-4,
+                               lr_schedule=lr_mod.for_dataset("cifar10"), use_graph=True, allreduce="rccl")
+        assert sess.engine is not None and sess.engine.p2p is None and not sess.use_graph
+        sess.run(SyntheticFeeder(sess.ex, seed=0), [StopAtStepHook(24)])
+        loss = float(sess.ex.metrics()["cross_entropy"])
+        q.put((mode, sess.graph_choice, sess.global_step, sess.use_graph, sess.ex.side is not None, loss))
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((mode, repr(e) + traceback.format_exc(), None, None, None, None))
+
+
+@pytest.mark.timeout(300)
+def test_rccl_dp_session_times_eager_vs_segmented_graphs():
+    """Data parallel over RCCL (single-rank process group): the session's first steps time the
+    eager step and the chain of segmented graphs, keep the faster, and keep training in that mode
+    (DRN_DP_GRAPH=auto); DRN_DP_GRAPH=0 stays eager with no trial."""
+    ctx = mp.get_context("spawn")
+    for mode in ("auto", "0"):
+        q = ctx.Queue()
+        p = ctx.Process(target=_trial_worker, args=(_free_port(), q, mode))
+        p.start()
+        m, choice, step, graph, side, loss = q.get(timeout=280)
+        p.join(timeout=60)
+        assert not isinstance(choice, str), choice
+        assert step == 24 and loss == loss, (step, loss)
+        if mode == "auto":
+            assert choice is not None and choice["eager_ms"] > 0 and choice["graph_ms"] > 0, choice
+            assert graph == (choice["mode"] == "segmented graphs")
+            assert side == (not graph)  # eager keeps the weight-gradient side stream
+        else:
+            assert choice is None and not graph and side

@@ -846,6 +846,33 @@ def test_bn_consumer_finalize(hip, ref, C, G, relu_bwd):
         assert rel(a, b) < 1e-2, name
 
 
+@pytest.mark.parametrize("C", [256, 1024])
+def test_bn_bwd_apply_fin_non_publishing(hip, C):
+    """A non-publishing backward apply (fused prologue finalize below BN_FIN_SPLIT_C channels,
+    separate finalize launch into scratch at and above it) leaves dgamma / dbeta untouched and
+    computes the same dx as the publishing one."""
+    from distributed_resnet_tensorflow_amd.ops.backend import BnCfin
+    torch.manual_seed(13)
+    N, H = 4, 6
+    M = N * H * H
+    x = bf(torch.randn(N, H, H, C)).cuda()
+    dy = bf(torch.randn(N, H, H, C)).cuda()
+    sc, sh = (torch.rand(C) + 0.5).cuda(), (torch.randn(C) * 0.3).cuda()
+    mu, isd = (torch.randn(C) * 0.1).cuda(), (torch.rand(C) + 0.5).cuda()
+    bst = torch.randn(4, 2, C).cuda()
+    gamma = (torch.rand(C) + 0.5).cuda()
+    res = {}
+    for pub in (True, False):
+        dg, db = torch.full((C,), 7.0, device="cuda"), torch.full((C,), 7.0, device="cuda")
+        dx = torch.zeros_like(x)
+        hip.bn_bwd_apply_fin(dy, None, 0, x, sc, sh, BnCfin(bst, float(M), gamma, mean=mu, invstd=isd, dgamma=dg,
+                                                           dbeta=db, publish=pub), None, dx, relu=True)
+        res[pub] = (dx.float().cpu(), dg.cpu(), db.cpu())
+    assert torch.equal(res[True][0], res[False][0])
+    assert bool((res[False][1] == 7.0).all()) and bool((res[False][2] == 7.0).all())
+    assert not bool((res[True][1] == 7.0).all())
+
+
 @pytest.mark.parametrize("publish", [True, False])
 @pytest.mark.parametrize("nk", [False, True])
 def test_conv_prologue_finalize(hip, ref, publish, nk):
