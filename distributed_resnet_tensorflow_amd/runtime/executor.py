@@ -806,6 +806,8 @@ class Executor:
             tgt = bufs[tgt_k]
             a_in, pro = (b.act, None) if b.act is not None else (b.src, b.ss)
             self._wgrad(a_in, dy, op.dw, op.geom, in_bn=pro, dy_buf=dy_buf, bnb=lazy)
+            if i == 0 and bp.proj is not None:
+                self._wgrad(a_in, d_out, bp.proj.dw, bp.proj.geom, in_bn=pro, dy_buf=bufs[cur])
             self._claim(tgt)
             da = self._view(tgt, xin)        # d relu(bn(xin))
             add = None
@@ -814,7 +816,6 @@ class Executor:
                 # the projection's data gradient first, the main conv's accumulating one last so
                 # that its (full-cover, stride-1) epilogue can carry the fused BN reduction
                 pj = bp.proj
-                self._wgrad(a_in, d_out, pj.dw, pj.geom, in_bn=pro, dy_buf=bufs[cur])
                 self._dgrad(pj, d_out, da, accumulate=False)
                 self._dgrad(op, dy, da, accumulate=True, bn=b if fuse else None, bn_x=xin, bnb=lazy)
             else:
