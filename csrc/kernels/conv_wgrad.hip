@@ -282,20 +282,6 @@ __global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_wgrad_kernel(DrnCo
   wgrad_store<MI, MJ>(a, acc, split, c0 + wc * WCO, k0 + wk * WKK, Ktot, lane);
 }
 
-// Minimum dynamic LDS per weight-gradient workgroup (DRN_WGRAD_LDS_MIN, bytes; default 0): a
-// floor above 80 KB keeps ONE weight-gradient workgroup per CU, so a data-gradient workgroup of
-// the main stream always finds room beside it instead of waiting for a side-stream workgroup
-// to retire (the weight gradients run concurrently with the critical-path chain).
-static int wgrad_lds(int need) {
-  static int floor_ = -1;
-  if (floor_ < 0) {
-    const char* e = getenv("DRN_WGRAD_LDS_MIN");
-    floor_ = e ? atoi(e) : 0;
-    if (floor_ < 0 || floor_ > 160 * 1024) floor_ = 0;
-  }
-  return need > floor_ ? need : floor_;
-}
-
 template <int BKK, int BCO, bool PRO>
 static int launch_wgrad(DrnConvWgradArgs* a, hipStream_t s) {
   constexpr int NST = DRN_WGRAD_STAGES;
@@ -303,13 +289,13 @@ static int launch_wgrad(DrnConvWgradArgs* a, hipStream_t s) {
   static bool attr_set = false;
   auto kern = conv_wgrad_kernel<BKK, BCO, PRO, NST>;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
   }
   const int Ktot = a->R * a->S * a->C;
   const int nkt = (Ktot + BKK - 1) / BKK;
   const int nct = (a->K + BCO - 1) / BCO;
-  hipLaunchKernelGGL(kern, dim3(nkt * nct, a->splits), dim3(256), wgrad_lds(LDS), s, *a);
+  hipLaunchKernelGGL(kern, dim3(nkt * nct, a->splits), dim3(256), LDS, s, *a);
   return (int)hipGetLastError();
 }
 
@@ -865,13 +851,13 @@ static int launch_wgrad_glds_p(DrnConvWgradArgs* a, const void* zero, hipStream_
   static bool attr_set = false;
   auto kern = conv_wgrad_glds_kernel<BKK, BCO, NS, BP, PRO, BNB, IL, LIN>;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
   }
   const int Ktot = a->R * a->S * a->C;
   const int nkt = (Ktot + BKK - 1) / BKK;
   const int nct = (a->K + BCO - 1) / BCO;
-  hipLaunchKernelGGL(kern, dim3(nkt * nct, a->splits), dim3(256), wgrad_lds(LDS), s, *a, zero);
+  hipLaunchKernelGGL(kern, dim3(nkt * nct, a->splits), dim3(256), LDS, s, *a, zero);
   return (int)hipGetLastError();
 }
 
