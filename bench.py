@@ -237,6 +237,7 @@ def main():
     if os.environ.get("DRN_PRINT_TUNE") == "1" and rank == 0:
         for key, cfg, us in be.tune_log:
             print(f"[tune] {key} -> {cfg} ({us} us)", file=sys.stderr)
+        print(f"[tune] in-situ re-timing changed {getattr(be, 'insitu_changed', 0)} conv choices", file=sys.stderr)
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()

@@ -259,6 +259,8 @@ class HipBackend(_Common):
         self.tune_cold = os.environ.get("DRN_TUNE_COLD", "0") == "1"
         self._evict_buf = None
         self._fin_bufs: dict = {}
+        self.conv_cands: dict = {}   # geometry key -> tuner finalists, fastest first
+        self._insitu = None          # list of (key, cfg, ev0, ev1) while Executor.insitu_tune runs
 
     def _timed(self, launch, n: int) -> float:
         """Mean ms of n launches of launch() on the current stream (cold: one L2 eviction before
@@ -404,7 +406,19 @@ class HipBackend(_Common):
             cfg, ks = self.conv_cfg.get(key, (-1, 1))
             a.cfg = cfg
             self._set_ksplit(a, ks)
+        if self._insitu is not None:   # in-situ re-timing (Executor.insitu_tune): events around it
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            _lib.check(self.L.drn_conv_fwd2(ctypes.byref(a), self.zero_page.data_ptr(), self.stream()), "drn_conv_fwd")
+            e1.record()
+            self._insitu.append((self.conv_key(a), (int(a.cfg), self._ks_of(a)), e0, e1))
+            return
         _lib.check(self.L.drn_conv_fwd2(ctypes.byref(a), self.zero_page.data_ptr(), self.stream()), "drn_conv_fwd")
+
+    @staticmethod
+    def _ks_of(a) -> int:
+        """The split-K / stream-K factor a launch was configured with (inverse of _set_ksplit)."""
+        return -int(a.sk_blocks) if a.sk_blocks else (int(a.ksplit) if a.ksplit > 1 else 1)
 
     def _tune_conv(self, a, key, iters: int = 0) -> int:
         """Time every kernel configuration for this geometry (the MIOpen 'find' step, done once
@@ -481,6 +495,8 @@ class HipBackend(_Common):
                 top[c] = min(top[c], time_cfg(c, 2 * iters))
         best, best_t = min(top.items(), key=lambda kv: kv[1]) if top else ((100, 1), 0.0)
         self.tune_log.append((key, best, round(best_t * 1e3, 1)))
+        # the finalists, fastest first: Executor.insitu_tune re-times them inside a real step
+        self.conv_cands[key] = [c for c, _ in sorted(top.items(), key=lambda kv: kv[1])]
         return best
 
     def conv_fwd(self, x, w, y, g, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None, bn_bwd=None,

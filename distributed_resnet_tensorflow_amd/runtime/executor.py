@@ -937,8 +937,57 @@ class Executor:
         self.P.grad.zero_()
         if self.is_hip:
             torch.cuda.synchronize()
+            if os.environ.get("DRN_INSITU_TUNE", "1") == "1":
+                self.insitu_tune()
             if hasattr(self.be, "save_tune_db"):
                 self.be.save_tune_db()   # persist newly timed kernel choices (ops/tunedb.py)
+
+    def insitu_tune(self, rounds: int = 2):
+        """Re-time the autotuner's finalists of every forward / data-gradient conv INSIDE real
+        forward + backward passes (weight gradients running beside them on the side stream, the
+        operands as the previous kernel left them in the caches) and keep, per geometry, the one
+        with the least in-step time. The isolated tuner times a kernel re-launched on L2-warm
+        operands on an idle GPU; in the step some layers ran ~30 % slower than their isolated
+        time, and not always with the same ranking. Events bracket each conv launch only while
+        this runs; BN moving statistics and gradients are restored afterwards."""
+        be = self.be
+        cands = {k: v for k, v in getattr(be, "conv_cands", {}).items() if len(v) > 1}
+        if not cands:
+            return
+        saved = self.P.bn_state.clone()
+        hook, self.grad_ready = self.grad_ready, None
+        width = max(len(v) for v in cands.values())
+        best = {k: {} for k in cands}
+        for _ in range(rounds):
+            for r in range(width):
+                for k, v in cands.items():
+                    be.conv_cfg[k] = v[r % len(v)]
+                be._insitu = []
+                try:
+                    self.forward(train=True)
+                    self.backward()
+                    torch.cuda.synchronize()
+                    sums = {}
+                    for key, cfg, e0, e1 in be._insitu:
+                        if key in best:
+                            sums[(key, cfg)] = sums.get((key, cfg), 0.0) + e0.elapsed_time(e1)
+                finally:
+                    be._insitu = None
+                for (key, cfg), ms in sums.items():
+                    best[key][cfg] = min(best[key].get(cfg, float("inf")), ms)
+        changed = 0
+        for k, times in best.items():
+            pick = min(times.items(), key=lambda kv: kv[1])[0] if times else cands[k][0]
+            changed += pick != cands[k][0]
+            be.conv_cfg[k] = pick
+            if hasattr(be, "tune_db"):
+                be.tune_db().put_conv(k, pick)
+        be.insitu_changed = changed
+        be.conv_cands = {}
+        self.grad_ready = hook
+        self.P.bn_state.copy_(saved)
+        self.P.grad.zero_()
+        torch.cuda.synchronize()
 
     def train_step(self, lr: Optional[float] = None, grad_scale: float = 1.0, allreduce: Optional[Callable] = None):
         if lr is not None:
