@@ -30,15 +30,14 @@ __global__ __launch_bounds__(256) void sgd_momentum_kernel(float* __restrict__ w
   // skip: the step's gradient exchange failed (P2P error word): apply no update at all
   if (skip != nullptr && *skip != 0) return;
   const float lr = *lr_ptr;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    float4 wv = reinterpret_cast<float4*>(w)[i];
-    float4 mv = reinterpret_cast<float4*>(m)[i];
-    const float4 gv = grad4(g, i);
+  auto upd = [&](float4& wv, float4& mv, const float4& gv) {
     float gg;
     gg = gv.x * grad_scale + wd * wv.x; mv.x = mu * mv.x + gg; wv.x -= lr * mv.x;
     gg = gv.y * grad_scale + wd * wv.y; mv.y = mu * mv.y + gg; wv.y -= lr * mv.y;
     gg = gv.z * grad_scale + wd * wv.z; mv.z = mu * mv.z + gg; wv.z -= lr * mv.z;
     gg = gv.w * grad_scale + wd * wv.w; mv.w = mu * mv.w + gg; wv.w -= lr * mv.w;
+  };
+  auto store = [&](int64_t i, const float4& wv, const float4& mv) {
     reinterpret_cast<float4*>(w)[i] = wv;
     reinterpret_cast<float4*>(m)[i] = mv;
     if (wb) {
@@ -47,6 +46,26 @@ __global__ __launch_bounds__(256) void sgd_momentum_kernel(float* __restrict__ w
       o.y = pack2bf(wv.z, wv.w);
       reinterpret_cast<uint2*>(wb)[i] = o;
     }
+  };
+  // two float4 groups in flight per thread (3 streams read, 3 written: one group per iteration
+  // left the pass latency-bound at ~4.3 TB/s)
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  for (; i + stride < n4; i += 2 * stride) {
+    float4 w0 = reinterpret_cast<float4*>(w)[i], w1 = reinterpret_cast<float4*>(w)[i + stride];
+    float4 m0 = reinterpret_cast<float4*>(m)[i], m1 = reinterpret_cast<float4*>(m)[i + stride];
+    const float4 g0 = grad4(g, i), g1 = grad4(g, i + stride);
+    upd(w0, m0, g0);
+    upd(w1, m1, g1);
+    store(i, w0, m0);
+    store(i + stride, w1, m1);
+  }
+  if (i < n4) {
+    float4 w0 = reinterpret_cast<float4*>(w)[i];
+    float4 m0 = reinterpret_cast<float4*>(m)[i];
+    const float4 g0 = grad4(g, i);
+    upd(w0, m0, g0);
+    store(i, w0, m0);
   }
 }
 
