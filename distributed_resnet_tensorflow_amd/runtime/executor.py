@@ -938,7 +938,7 @@ class Executor:
         if self.is_hip:
             torch.cuda.synchronize()
             if os.environ.get("DRN_INSITU_TUNE", "1") == "1":
-                self.insitu_tune()
+                self.insitu_tune(rounds=int(os.environ.get("DRN_INSITU_ROUNDS", "2")))
             if hasattr(self.be, "save_tune_db"):
                 self.be.save_tune_db()   # persist newly timed kernel choices (ops/tunedb.py)
 

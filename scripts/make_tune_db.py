@@ -11,7 +11,8 @@ import os
 import sys
 
 os.environ.setdefault("DRN_TUNE_ITERS", "20")
-os.environ.setdefault("DRN_TUNE_TOP", "6")
+os.environ.setdefault("DRN_TUNE_TOP", "4")        # (more finalists made the in-situ pick noisier)
+os.environ.setdefault("DRN_INSITU_ROUNDS", "3")
 os.environ.setdefault("DRN_TUNE_ROUNDS", "4")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
