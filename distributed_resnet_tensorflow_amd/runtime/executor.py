@@ -157,7 +157,17 @@ class Executor:
         self.claim_query = os.environ.get("DRN_CLAIM_QUERY", "1") == "1"
         if self.is_hip and os.environ.get("DRN_WGRAD_STREAM", "1") == "1":
             self.side = torch.cuda.Stream(self.device)
+        # gradient-buffer reuse guard: id(buffer) -> sequence number of the side-stream weight
+        # gradient that last read it; _marks[seq] = event recorded after that weight gradient;
+        # the main stream has waited for the side stream up to _synced
         self._pending = {}
+        self._marks = {}
+        self._wseq = 0
+        self._synced = 0
+        # a claim that needs a wait waits on the side-stream mark up to claim_lag weight gradients
+        # behind the newest one (covering the claims of the next few blocks with ONE cross-queue
+        # barrier instead of one per data gradient: each barrier packet stalls the main queue)
+        self.claim_lag = int(os.environ.get("DRN_CLAIM_LAG", "6"))
         # BN-apply+ReLU either fused into every consuming conv's load prologue (recomputed by the
         # forward conv, the projection conv and both weight-gradient convs; the LDS-DMA kernels
         # rewrite each landed stage in LDS before its barrier) or materialised once per BN by a
@@ -672,6 +682,8 @@ class Executor:
         self._report(self.P.by_name[f"{fb.bn.name}/gamma"].offset)
         cur = self._lru[-1]  # index of the buffer holding d_out
         self._pending.clear()
+        self._marks.clear()
+        self._wseq = self._synced = 0
         if self._tflip_ev is not None:  # the flipped weights refreshed on the side stream
             # (a capture starts after its eager warm-up has synchronized: the event is complete,
             # and a graph may not wait on an event recorded outside it)
@@ -745,19 +757,27 @@ class Executor:
             if post is not None:
                 post()
         if dy_buf is not None:                           # the main stream must not overwrite dy early
+            self._wseq += 1
             ev = torch.cuda.Event()
             ev.record(self.side)
-            self._pending[id(dy_buf)] = ev
+            self._marks[self._wseq] = ev
+            self._pending[id(dy_buf)] = self._wseq
 
     def _claim(self, buf):
         """Before the main stream writes a rotating gradient buffer: wait for the side-stream
         weight gradient still reading it."""
-        ev = self._pending.pop(id(buf), None)
-        if ev is None:
-            return
-        # an event that has already completed needs no cross-queue barrier packet (each one
-        # costs the main queue a few us before the next kernel starts); inside a capture the
-        # dependency must be recorded as a graph edge regardless
+        seq = self._pending.pop(id(buf), None)
+        if seq is None or seq <= self._synced:
+            return                       # an earlier wait already ordered main after that reader
+        # (the side stream runs in order: waiting on a later mark covers every earlier reader)
+        target = max(seq, self._wseq - self.claim_lag)
+        s = max(k for k in self._marks if seq <= k <= target)
+        ev = self._marks[s]
+        self._synced = s
+        for k in [k for k in self._marks if k < s]:
+            del self._marks[k]
+        # an event that has already completed needs no cross-queue barrier packet; inside a
+        # capture the dependency must be recorded as a graph edge regardless
         if self.claim_query and not torch.cuda.is_current_stream_capturing() and ev.query():
             return
         torch.cuda.current_stream(self.device).wait_event(ev)
@@ -769,6 +789,8 @@ class Executor:
         if ev is None:
             main.wait_stream(self.side)
             self._pending.clear()
+            self._marks.clear()
+            self._synced = self._wseq
         else:
             main.wait_event(ev)
 
