@@ -164,10 +164,11 @@ class Executor:
         self._marks = {}
         self._wseq = 0
         self._synced = 0
-        # a claim that needs a wait waits on the side-stream mark up to claim_lag weight gradients
-        # behind the newest one (covering the claims of the next few blocks with ONE cross-queue
-        # barrier instead of one per data gradient: each barrier packet stalls the main queue)
-        self.claim_lag = int(os.environ.get("DRN_CLAIM_LAG", "6"))
+        # a claim that needs a wait waits on the side-stream mark up to claim_span weight
+        # gradients AFTER the buffer's reader (still many blocks old, so normally complete when
+        # the main stream gets there): it covers the next claims too -- one cross-queue barrier
+        # packet per claim_span claims instead of one per data gradient
+        self.claim_span = int(os.environ.get("DRN_CLAIM_SPAN", "12"))
         # BN-apply+ReLU either fused into every consuming conv's load prologue (recomputed by the
         # forward conv, the projection conv and both weight-gradient convs; the LDS-DMA kernels
         # rewrite each landed stage in LDS before its barrier) or materialised once per BN by a
@@ -770,7 +771,7 @@ class Executor:
         if seq is None or seq <= self._synced:
             return                       # an earlier wait already ordered main after that reader
         # (the side stream runs in order: waiting on a later mark covers every earlier reader)
-        target = max(seq, self._wseq - self.claim_lag)
+        target = seq + self.claim_span
         s = max(k for k in self._marks if seq <= k <= target)
         ev = self._marks[s]
         self._synced = s
