@@ -253,42 +253,24 @@ class HipBackend(_Common):
         self.tune_iters = int(os.environ.get("DRN_TUNE_ITERS", "5"))
         self.tune_top = int(os.environ.get("DRN_TUNE_TOP", "4"))
         self.tune_rounds = int(os.environ.get("DRN_TUNE_ROUNDS", "2"))
-        # cold timing: every timed launch follows a 64 MB scratch write that evicts the L2s (the
-        # operands stay in the Infinity Cache) -- inside a training step a conv reads what the
-        # previous kernel wrote from other XCDs, never its own L2-warm copy of a re-launched input
-        self.tune_cold = os.environ.get("DRN_TUNE_COLD", "0") == "1"
-        self._evict_buf = None
         self._fin_bufs: dict = {}
         self.conv_cands: dict = {}   # geometry key -> tuner finalists, fastest first
         self._insitu = None          # list of (key, cfg, ev0, ev1) while Executor.insitu_tune runs
 
     def _timed(self, launch, n: int) -> float:
-        """Mean ms of n launches of launch() on the current stream (cold: one L2 eviction before
-        each, bracketed per launch so the eviction is not timed)."""
-        if not self.tune_cold:
-            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            ev0.record()
-            for _ in range(n):
-                launch()
-            ev1.record()
-            ev1.synchronize()
-            return ev0.elapsed_time(ev1) / n
-        if self._evict_buf is None:
-            self._evict_buf = torch.empty(16 << 20, dtype=torch.float32, device=self.device)
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
-        for e0, e1 in evs:
-            self._evict_buf.zero_()
-            e0.record()
+        """Mean ms of n back-to-back launches of launch() on the current stream."""
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        for _ in range(n):
             launch()
-            e1.record()
-        evs[-1][1].synchronize()
-        return sum(e0.elapsed_time(e1) for e0, e1 in evs) / n
+        ev1.record()
+        ev1.synchronize()
+        return ev0.elapsed_time(ev1) / n
 
     def tune_db(self):
         if self._db is None:
             from .tunedb import TuneDB, section_for
-            # (cold- and warm-timed choices differ: the timing mode is part of the section)
-            self._db = TuneDB(section_for(self.device, self.L) + ("-cold" if self.tune_cold else ""))
+            self._db = TuneDB(section_for(self.device, self.L))
         return self._db
 
     def save_tune_db(self) -> bool:
