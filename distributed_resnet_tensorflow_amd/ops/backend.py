@@ -731,7 +731,7 @@ class HipBackend(_Common):
     # reads in its prologue (2048 workgroups x 2048 channels x 64 B = 268 MB at the last stage of
     # ResNet-50): from this many channels on, one small finalize launch computes the
     # coefficients once and the apply reads only its own 8 channels'
-    BN_FIN_SPLIT_C = int(os.environ.get("DRN_BN_FIN_SPLIT_C", "512"))
+    BN_FIN_SPLIT_C = int(os.environ.get("DRN_BN_FIN_SPLIT_C", "1024"))
 
     def _fin_scratch(self, C: int) -> torch.Tensor:
         """[coef 3C][dgamma C][dbeta C] fp32 scratch of the split backward finalize (one per C:
