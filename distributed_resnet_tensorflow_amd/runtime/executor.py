@@ -771,7 +771,9 @@ class Executor:
         if seq is None or seq <= self._synced:
             return                       # an earlier wait already ordered main after that reader
         # (the side stream runs in order: waiting on a later mark covers every earlier reader)
-        target = seq + self.claim_span
+        # (never closer than claim_span marks to the newest one: with a small buffer pool -- CIFAR
+        # keeps 6 -- the reader is recent and the wait must not extend to the newest marks)
+        target = max(seq, min(seq + self.claim_span, self._wseq - self.claim_span))
         s = max(k for k in self._marks if seq <= k <= target)
         ev = self._marks[s]
         self._synced = s
