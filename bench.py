@@ -185,6 +185,19 @@ def main():
                 t_eager, t_graph = tt.tolist()
             if t_eager < t_graph:
                 run, use_graph = eager, 0
+            elif eng is None and ex.side is not None:
+                # the graph candidate without the weight-gradient side stream (one stream: CIFAR
+                # ResNet-50 bs32 1.585 vs 1.785 ms; the side stream wins for larger steps)
+                side, ex.side = ex.side, None
+                sg1 = StepGraph(step, warmup=2)
+                t_one = float("inf")
+                for _ in range(3):
+                    t_one = min(t_one, _time(sg1.replay))
+                if t_one < t_graph:
+                    run = sg1.replay
+                else:
+                    ex.side = side
+                    del sg1
     for _ in range(args.warmup):
         run()
     torch.cuda.synchronize()
@@ -230,7 +243,8 @@ def main():
             "data": "synthetic (random-init weights, fixed synthetic batch of the benchmark shape)",
             "config": {"model": model, "global_batch": args.batch_size * world, "per_gpu_batch": args.batch_size,
                        "image_size": spec.image_size, "num_classes": spec.num_classes,
-                       "parallelism": f"dp{world}", "hip_graph": bool(use_graph)},
+                       "parallelism": f"dp{world}", "hip_graph": bool(use_graph),
+                       "wgrad_side_stream": ex.side is not None},
             "final_loss": round(loss, 4),
         }
         print(json.dumps(out), file=result_out, flush=True)

@@ -43,6 +43,20 @@ def make_backend(device: str, precision: str = "bf16"):
     return RefBackend("cpu")
 
 
+class _LazyGraph:
+    """Placeholder graph: its first replay() captures the step (the StepGraph warm-up is that
+    real step), later replays run the captured graph."""
+
+    def __init__(self, sess):
+        self.sess, self.g = sess, None
+
+    def replay(self):
+        if self.g is None:
+            self.g = StepGraph(self.sess._step_body, warmup=1)
+        else:
+            self.g.replay()
+
+
 class TrainingSession:
     def __init__(self, spec, batch: int, cluster, *, weight_decay: float, lr_schedule, checkpoint_dir: str = "",
                  max_to_keep: int = 5, seed: int = 0, use_graph: bool = True, sync_mode: str = "sync",
@@ -102,6 +116,13 @@ class TrainingSession:
         self._trial = ["eager", 0, 0.0, 0.0] if (use_graph and hip_cuda and dp_ok and self.engine.p2p is None
                                                 and dp_graph == "auto") else None
         self.graph_choice: Optional[dict] = None
+        # single-GPU graph step: its first replays time the step with and without the weight-
+        # gradient side stream and keep the faster (CIFAR ResNet-50 bs32: one stream 1.585 ms vs
+        # 1.785 ms; ImageNet bs128 and CIFAR bs128: the side stream wins) -- DRN_SIDE_TRIAL=0 off
+        self._strial = None
+        self._side_trial = (self.use_graph and self.engine is None and self.ex.side is not None
+                            and os.environ.get("DRN_SIDE_TRIAL", "1") == "1")
+        self.side_choice: Optional[dict] = None
         if not self.use_graph and self.device.type == "cuda" and self.be.name == "hip":
             # eager step (data parallel or not): the critical path on its own high-priority HW
             # queue, ahead of the weight-gradient side stream (ResNet-50 bs128 on one GPU: 9.93 vs
@@ -180,6 +201,8 @@ class TrainingSession:
                     self._graph = SegmentedStepGraph(self.ex, self.engine, 1.0 / self.world, warmup=1)
                 else:
                     self._graph = StepGraph(self._step_body, warmup=1)
+                    if self._side_trial:
+                        self._strial = ["side", 0, 0.0, 0.0, None]
             else:
                 if self.engine is not None:
                     self.engine.replay_begin()
@@ -187,6 +210,8 @@ class TrainingSession:
                     self._graph.replay()
                 if self.engine is not None:
                     self.engine.replay_end()
+                if self._strial is not None:
+                    self._side_trial_tick()
         elif self._trial is not None and not self.ex.check_nan:
             self._trial_step()
         else:
@@ -244,6 +269,36 @@ class TrainingSession:
                     self._trial = None
                     return
         tr[1] = n + 1
+
+    def _side_trial_tick(self):
+        """After each REAL graph-replayed step of the side-stream trial: TRIAL_WARM replays, then
+        TRIAL_STEPS timed ones with the side stream; the next step captures the step without it
+        (its eager warm-up is a real step), times it the same way and keeps the faster graph."""
+        tr = self._strial
+        W, K = self.TRIAL_WARM, self.TRIAL_STEPS
+        tr[1] += 1
+        if tr[1] == W:
+            torch.cuda.synchronize(self.device)
+            tr[2] = time.perf_counter()
+        if tr[1] < W + K:
+            return
+        torch.cuda.synchronize(self.device)
+        ms = (time.perf_counter() - tr[2]) / K * 1e3
+        if tr[0] == "side":
+            # the next step: capture without the side stream (StepGraph's warm-up = that step)
+            tr[0], tr[1], tr[3], tr[4] = "noside", 0, ms, (self._graph, self.ex.side)
+            self.ex.side = None
+            self._graph = _LazyGraph(self)
+            return
+        side_graph, side_stream = tr[4]
+        keep = ms < tr[3]
+        self.side_choice = {"side_ms": round(tr[3], 3), "one_stream_ms": round(ms, 3),
+                            "mode": "one stream" if keep else "weight-gradient side stream"}
+        log.info("graph step: side stream %.3f ms, one stream %.3f ms -> %s", tr[3], ms, self.side_choice["mode"])
+        if not keep:
+            self.ex.side = side_stream
+            self._graph = side_graph
+        self._strial = None
 
     def _guard(self, fn):
         """Run an error check; on failure mark the session failed (no checkpoint after it)."""

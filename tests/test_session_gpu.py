@@ -1,0 +1,35 @@
+"""Single-GPU TrainingSession: the graph step's side-stream trial (train/session.py).
+
+The first replays of the captured step are timed with the weight-gradient side stream, the
+step is then re-captured on one stream and timed the same way, and the faster graph is kept;
+every replay is a real training step, so training continues without a gap and the global step
+counts every one of them."""
+import pytest
+import torch
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")]
+
+
+@pytest.mark.parametrize("trial", ["1", "0"])
+def test_graph_step_side_stream_trial(monkeypatch, trial):
+    monkeypatch.setenv("DRN_SIDE_TRIAL", trial)
+    from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2
+    from distributed_resnet_tensorflow_amd.parallel.cluster import ClusterInfo
+    from distributed_resnet_tensorflow_amd.train import lr as lr_mod
+    from distributed_resnet_tensorflow_amd.train.feeder import SyntheticFeeder
+    from distributed_resnet_tensorflow_amd.train.hooks import StopAtStepHook
+    from distributed_resnet_tensorflow_amd.train.session import TrainingSession
+    sess = TrainingSession(cifar_resnet_v2(8), 16, ClusterInfo(device="cuda:0"), weight_decay=2e-4,
+                           lr_schedule=lr_mod.for_dataset("cifar10"), use_graph=True)
+    assert sess.use_graph and sess.engine is None and sess.ex.side is not None
+    sess.run(SyntheticFeeder(sess.ex, seed=0), [StopAtStepHook(30)])
+    torch.cuda.synchronize()
+    assert sess.global_step == 30
+    loss = float(sess.ex.metrics()["cross_entropy"])
+    assert loss == loss
+    if trial == "1":
+        c = sess.side_choice
+        assert c is not None and c["side_ms"] > 0 and c["one_stream_ms"] > 0, c
+        assert (sess.ex.side is None) == (c["mode"] == "one stream")
+    else:
+        assert sess.side_choice is None and sess.ex.side is not None
