@@ -254,6 +254,13 @@ class DataParallelEngine:
             if not self.launched[i] and lo >= self.frontier:
                 self._launch(i)
 
+    def launches_at(self, lo_ready: int) -> bool:
+        """Whether a grad_ready(lo_ready) report would launch a bucket (the executor orders the
+        report after the main stream only then: a report that launches nothing needs no
+        cross-stream wait)."""
+        f = min(self.frontier, lo_ready)
+        return any(not self.launched[i] and lo >= f for i, (lo, _) in enumerate(self.buckets))
+
     def _mark(self, k: int):
         if self._ev is not None:
             self._ev[k].record()

@@ -738,6 +738,10 @@ class Executor:
         if self.side is None:
             self.grad_ready(lo)
             return
+        owner = getattr(self.grad_ready, "__self__", None)
+        if owner is not None and hasattr(owner, "launches_at") and not owner.launches_at(lo):
+            self.grad_ready(lo)                          # (advances the frontier, launches nothing)
+            return
         self.side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.side):
             self.grad_ready(lo)
