@@ -185,7 +185,7 @@ def main():
                 t_eager, t_graph = tt.tolist()
             if t_eager < t_graph:
                 run, use_graph = eager, 0
-            elif eng is None and ex.side is not None:
+            elif (eng is None or eng.p2p is not None) and ex.side is not None:
                 # the graph candidate without the weight-gradient side stream (one stream: CIFAR
                 # ResNet-50 bs32 1.585 vs 1.785 ms; the side stream wins for larger steps)
                 side, ex.side = ex.side, None
@@ -193,6 +193,11 @@ def main():
                 t_one = float("inf")
                 for _ in range(3):
                     t_one = min(t_one, _time(sg1.replay))
+                if world > 1:  # every rank takes the same decision (the slowest rank's timings)
+                    tt = torch.tensor([t_one, t_graph], dtype=torch.float64,
+                                      device="cuda" if backend == "nccl" else "cpu")
+                    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                    t_one, t_graph = tt.tolist()
                 if t_one < t_graph:
                     run = sg1.replay
                 else:

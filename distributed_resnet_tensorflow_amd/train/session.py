@@ -120,8 +120,10 @@ class TrainingSession:
         # gradient side stream and keep the faster (CIFAR ResNet-50 bs32: one stream 1.585 ms vs
         # 1.785 ms; ImageNet bs128 and CIFAR bs128: the side stream wins) -- DRN_SIDE_TRIAL=0 off
         self._strial = None
-        self._side_trial = (self.use_graph and self.engine is None and self.ex.side is not None
-                            and os.environ.get("DRN_SIDE_TRIAL", "1") == "1")
+        # (also for the data-parallel P2P graph step: its reductions run on the P2P comm stream
+        # either way, only the weight gradients move)
+        self._side_trial = (self.use_graph and (self.engine is None or self.engine.p2p is not None)
+                            and self.ex.side is not None and os.environ.get("DRN_SIDE_TRIAL", "1") == "1")
         self.side_choice: Optional[dict] = None
         if not self.use_graph and self.device.type == "cuda" and self.be.name == "hip":
             # eager step (data parallel or not): the critical path on its own high-priority HW
@@ -204,11 +206,13 @@ class TrainingSession:
                     if self._side_trial:
                         self._strial = ["side", 0, 0.0, 0.0, None]
             else:
-                if self.engine is not None:
+                # (the trial's re-capture is an eager warm-up step: the engine brackets it itself)
+                hooks = self.engine is not None and not (isinstance(self._graph, _LazyGraph) and self._graph.g is None)
+                if hooks:
                     self.engine.replay_begin()
                 with phase("step (graph replay)"):
                     self._graph.replay()
-                if self.engine is not None:
+                if hooks:
                     self.engine.replay_end()
                 if self._strial is not None:
                     self._side_trial_tick()

@@ -33,3 +33,32 @@ def test_graph_step_side_stream_trial(monkeypatch, trial):
         assert (sess.ex.side is None) == (c["mode"] == "one stream")
     else:
         assert sess.side_choice is None and sess.ex.side is not None
+
+
+def test_p2p_dp_graph_step_side_stream_trial(monkeypatch):
+    """The same trial on the data-parallel step with the P2P all-reduce (single-rank engine,
+    whole step incl. the reductions in one graph): both candidates train, the global step counts
+    every real step, the P2P error word stays clear."""
+    monkeypatch.setenv("DRN_SIDE_TRIAL", "1")
+    monkeypatch.setenv("DRN_FORCE_DP", "1")
+    monkeypatch.setenv("DRN_FORCE_DP_PORT", "29611")
+    from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2
+    from distributed_resnet_tensorflow_amd.parallel.cluster import ClusterInfo
+    from distributed_resnet_tensorflow_amd.train import lr as lr_mod
+    from distributed_resnet_tensorflow_amd.train.feeder import SyntheticFeeder
+    from distributed_resnet_tensorflow_amd.train.hooks import StopAtStepHook
+    from distributed_resnet_tensorflow_amd.train.session import TrainingSession
+    import torch.distributed as dist
+    try:
+        sess = TrainingSession(cifar_resnet_v2(8), 16, ClusterInfo(device="cuda:0"), weight_decay=2e-4,
+                               lr_schedule=lr_mod.for_dataset("cifar10"), use_graph=True, allreduce="p2p")
+        assert sess.use_graph and sess.engine is not None and sess.engine.p2p is not None
+        sess.run(SyntheticFeeder(sess.ex, seed=0), [StopAtStepHook(30)])
+        torch.cuda.synchronize()
+        assert sess.global_step == 30 and sess.failed is None   # (run() polled the error word every step)
+        c = sess.side_choice
+        assert c is not None and c["side_ms"] > 0 and c["one_stream_ms"] > 0, c
+        assert float(sess.ex.metrics()["cross_entropy"]) == float(sess.ex.metrics()["cross_entropy"])
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
