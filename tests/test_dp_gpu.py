@@ -334,7 +334,7 @@ def _trial_worker(port, q, mode):
         sess = TrainingSession(cifar_resnet_v2(8), 32, ClusterInfo(device="cuda:0"), weight_decay=2e-4,
                                lr_schedule=lr_mod.for_dataset("cifar10"), use_graph=True, allreduce="rccl")
         assert sess.engine is not None and sess.engine.p2p is None and not sess.use_graph
-        sess.run(SyntheticFeeder(sess.ex, seed=0), [StopAtStepHook(24)])
+        sess.run(SyntheticFeeder(sess.ex, seed=0), [StopAtStepHook(40)])
         loss = float(sess.ex.metrics()["cross_entropy"])
         q.put((mode, sess.graph_choice, sess.global_step, sess.use_graph, sess.ex.side is not None, loss))
     except Exception as e:  # pragma: no cover
@@ -355,7 +355,7 @@ def test_rccl_dp_session_times_eager_vs_segmented_graphs():
         m, choice, step, graph, side, loss = q.get(timeout=280)
         p.join(timeout=60)
         assert not isinstance(choice, str), choice
-        assert step == 24 and loss == loss, (step, loss)
+        assert step == 40 and loss == loss, (step, loss)
         if mode == "auto":
             assert choice is not None and choice["eager_ms"] > 0 and choice["graph_ms"] > 0, choice
             assert graph == (choice["mode"] == "segmented graphs")

@@ -22,9 +22,9 @@ def test_graph_step_side_stream_trial(monkeypatch, trial):
     sess = TrainingSession(cifar_resnet_v2(8), 16, ClusterInfo(device="cuda:0"), weight_decay=2e-4,
                            lr_schedule=lr_mod.for_dataset("cifar10"), use_graph=True)
     assert sess.use_graph and sess.engine is None and sess.ex.side is not None
-    sess.run(SyntheticFeeder(sess.ex, seed=0), [StopAtStepHook(30)])
+    sess.run(SyntheticFeeder(sess.ex, seed=0), [StopAtStepHook(50)])
     torch.cuda.synchronize()
-    assert sess.global_step == 30
+    assert sess.global_step == 50
     loss = float(sess.ex.metrics()["cross_entropy"])
     assert loss == loss
     if trial == "1":
@@ -53,9 +53,9 @@ def test_p2p_dp_graph_step_side_stream_trial(monkeypatch):
         sess = TrainingSession(cifar_resnet_v2(8), 16, ClusterInfo(device="cuda:0"), weight_decay=2e-4,
                                lr_schedule=lr_mod.for_dataset("cifar10"), use_graph=True, allreduce="p2p")
         assert sess.use_graph and sess.engine is not None and sess.engine.p2p is not None
-        sess.run(SyntheticFeeder(sess.ex, seed=0), [StopAtStepHook(30)])
+        sess.run(SyntheticFeeder(sess.ex, seed=0), [StopAtStepHook(50)])
         torch.cuda.synchronize()
-        assert sess.global_step == 30 and sess.failed is None   # (run() polled the error word every step)
+        assert sess.global_step == 50 and sess.failed is None   # (run() polled the error word every step)
         c = sess.side_choice
         assert c is not None and c["side_ms"] > 0 and c["one_stream_ms"] > 0, c
         assert float(sess.ex.metrics()["cross_entropy"]) == float(sess.ex.metrics()["cross_entropy"])
