@@ -257,6 +257,7 @@ def main():
         for key, cfg, us in be.tune_log:
             print(f"[tune] {key} -> {cfg} ({us} us)", file=sys.stderr)
         print(f"[tune] in-situ re-timing changed {getattr(be, 'insitu_changed', 0)} conv choices", file=sys.stderr)
+        print(f"[tune] {be.db_hits} choices from the kernel-selection database", file=sys.stderr)
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()

@@ -56,11 +56,30 @@ def source_hash(kernels: Path = KERNELS, include: Path = INCLUDE) -> str:
     return h.hexdigest()
 
 
+# kernels whose code the tuner's choices depend on (the conv / weight-gradient / stem tiles and
+# their fused prologues / epilogues, all through the shared headers)
+TUNE_SOURCES = ("conv_fwd.hip", "conv_halo.hip", "conv_wgrad.hip", "stem.hip")
+
+
+def tune_hash(kernels: Path = KERNELS, include: Path = INCLUDE) -> str:
+    """sha256 over the sources the kernel-selection database depends on (TUNE_SOURCES + shared
+    headers): the database section key (ops/tunedb.py), so an edit of a pooling / optimizer /
+    BatchNorm-apply kernel does not throw away the shipped conv choices."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(kernels / n for n in TUNE_SOURCES) + sorted(include.glob("*.h")):
+        h.update(f.parent.name.encode() + b"/" + f.name.encode() + b"\0")
+        h.update(f.read_bytes())
+    return h.hexdigest()
+
+
 def _stamp_object() -> Path:
-    """A one-function translation unit returning source_hash(), rebuilt when the hash changes."""
+    """A translation unit returning source_hash() and tune_hash(), rebuilt when they change."""
     gen = OBJ_DIR / "drn_src_stamp.cc"
     text = ('extern "C" __attribute__((visibility("default"))) const char* drn_src_hash() '
-            f'{{ return "{source_hash()}"; }}\n')
+            f'{{ return "{source_hash()}"; }}\n'
+            'extern "C" __attribute__((visibility("default"))) const char* drn_tune_hash() '
+            f'{{ return "{tune_hash()}"; }}\n')
     if not gen.exists() or gen.read_text() != text:
         gen.write_text(text)
     obj = gen.with_suffix(".o")

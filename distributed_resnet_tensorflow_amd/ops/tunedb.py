@@ -9,8 +9,9 @@ start without the tuning pass.
 
 Entries are keyed by
   * the device architecture (gcnArchName, e.g. ``gfx950:sramecc+:xnack-``) and CU count,
-  * the kernel library's source hash (``drn_src_hash``, ops/build.py): a rebuilt library with
-    other kernels never reuses stale choices,
+  * the hash of the sources the choices depend on (``drn_tune_hash``, ops/build.py: the conv,
+    weight-gradient and stem kernels + shared headers): a library with other conv kernels never
+    reuses stale choices, while edits of unrelated kernels (pooling, SGD, BN applies) keep them,
   * the geometry key the backend already uses (conv_key / wgrad_key).
 
 File: ``DRN_TUNE_DB`` (``off`` disables it), default ``ops/tune_db.json`` next to the library, so
@@ -124,8 +125,10 @@ def section_for(device, lib_handle) -> str:
     props = torch.cuda.get_device_properties(device)
     arch = getattr(props, "gcnArchName", props.name)
     h = "nohash"
-    if hasattr(lib_handle, "drn_src_hash"):
-        f = lib_handle.drn_src_hash
-        f.restype, f.argtypes = ctypes.c_char_p, []
-        h = f().decode()[:16]
+    for sym in ("drn_tune_hash", "drn_src_hash"):  # tuning-relevant sources; older libraries: all
+        if hasattr(lib_handle, sym):
+            f = getattr(lib_handle, sym)
+            f.restype, f.argtypes = ctypes.c_char_p, []
+            h = f().decode()[:16]
+            break
     return f"{arch}/{props.multi_processor_count}cu|{h}"

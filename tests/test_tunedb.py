@@ -56,3 +56,32 @@ def test_disabled_by_env(tmp_path, monkeypatch):
     db = TuneDB("s|h")
     db.put_conv((1,), (3, 1))
     assert db.path is None and not db.save()
+
+
+def test_section_hash_covers_only_tuning_sources(tmp_path):
+    """The database section hash (build.tune_hash) follows the conv / weight-gradient / stem
+    kernels and the shared headers; editing another kernel changes the library hash only."""
+    from distributed_resnet_tensorflow_amd.ops import build
+    k, inc = tmp_path / "kernels", tmp_path / "include"
+    k.mkdir()
+    inc.mkdir()
+    for n in build.TUNE_SOURCES + ("pool.hip", "sgd.hip"):
+        (k / n).write_text(f"// {n}\n")
+    (inc / "drn_conv.h").write_text("// header\n")
+    t0, s0 = build.tune_hash(k, inc), build.source_hash(k, inc)
+    (k / "pool.hip").write_text("// pool, edited\n")
+    assert build.tune_hash(k, inc) == t0 and build.source_hash(k, inc) != s0
+    (k / "conv_wgrad.hip").write_text("// wgrad, edited\n")
+    assert build.tune_hash(k, inc) != t0
+    t1 = build.tune_hash(k, inc)
+    (inc / "drn_conv.h").write_text("// header, edited\n")
+    assert build.tune_hash(k, inc) != t1
+
+
+def test_shipped_database_matches_the_tree():
+    """The shipped database's section is keyed by the current tuning-source hash, so a bench run
+    on an MI355X uses it instead of re-tuning."""
+    from distributed_resnet_tensorflow_amd.ops import build
+    from distributed_resnet_tensorflow_amd.ops.tunedb import DEFAULT_PATH
+    secs = json.loads(DEFAULT_PATH.read_text())["sections"]
+    assert any(s.endswith("|" + build.tune_hash()[:16]) for s in secs), list(secs)
