@@ -1,5 +1,5 @@
-// drn_conv_epi.h -- device helpers shared by the implicit-GEMM convolution kernels
-// (conv_fwd.hip: LDS-DMA tile kernels; conv_halo.hip: halo-tiled direct 3x3 kernel): the fused
+// drn_conv_epi.h -- device helpers of the implicit-GEMM convolution kernels (conv_fwd.hip,
+// stem.hip): the fused
 // epilogue (LDS-staged fp32 tile -> coalesced bf16 rows, residual add, strided output map,
 // next-BN statistics or fused BN-backward reduction), the LDS-DMA issue helpers and the
 // swizzle of the 128-byte LDS rows.
@@ -170,9 +170,8 @@ __device__ __forceinline__ int epi_off(const DrnConvFwdArgs& a, int m, int c, in
   return ((n * a.out_H + i * a.out_stride + a.out_oh) * a.out_W + j * a.out_stride + a.out_ow) * a.K + c;
 }
 
-// Row map of the staged tile: staged row -> output pixel m (>= M: not an output pixel). The
-// implicit-GEMM kernels' tiles are consecutive pixels; the halo kernel's rows are 16-pixel
-// fragments of image rows (conv_halo.hip EpiRowHalo).
+// Row map of the staged tile: staged row -> output pixel m (>= M: not an output pixel); the
+// implicit-GEMM kernels' tiles are consecutive pixels.
 struct EpiRowId {
   __device__ __forceinline__ int operator()(int m0, int row) const { return m0 + row; }
 };

@@ -381,27 +381,61 @@ __device__ __forceinline__ void bn_bwd_fin_vec(const uint4& xv, float* fd, const
   }
 }
 
-template <bool ADD>
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(DySrc src, const bf16_t* __restrict__ x,
-                                                           const float* __restrict__ scale,
-                                                           const float* __restrict__ shift,
-                                                           const float* __restrict__ mean,
-                                                           const float* __restrict__ invstd,
-                                                           const float* __restrict__ coef,
-                                                           const bf16_t* __restrict__ add, bf16_t* __restrict__ dx,
-                                                           int64_t nvec, int C, int relu) {
-  // C/8 is a power of two (host-checked): the grid stride is a multiple of C/8, so every
-  // thread's 8 channels are fixed and all per-channel operands live in registers. The affine
-  // form dx = A*g + B*x + D folds k1*(g - k2 - (x-mu)*is*k3).
-  const int CV = C / 8;
-  const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int c = (int)(i0 & (CV - 1)) * 8;
+// Backward apply, shared by the two coefficient sources (FIN: finalized in the prologue from the
+// backward sums; else: the split finalize launch's coef[3][C] + the forward mean / invstd).
+// Latency structure (the f-channel tensors of stages 1-3 are 1-3 vectors per thread at 2048
+// workgroups): the thread's first U vectors of x / dy / add are issued BEFORE the coefficient
+// prologue, and every batch's successor is issued before the batch's stores, so the data
+// latency overlaps the finalize instead of following it. Out-of-range slots load a clamped
+// (valid) address and skip only the store: no per-element branch around a load (hipcc would
+// wait vmcnt(0) per element there).
+template <bool ADD, bool FIN, bool POOL>
+__device__ __forceinline__ void bn_bwd_apply_body(DySrc src, const bf16_t* __restrict__ x,
+                                                  const float* __restrict__ scale, const float* __restrict__ shift,
+                                                  const float* __restrict__ mean, const float* __restrict__ invstd,
+                                                  const float* __restrict__ coef, const DrnBnFin& f,
+                                                  const bf16_t* __restrict__ add, bf16_t* __restrict__ dx,
+                                                  int64_t nvec, int C, int relu, float* lsm) {
+  constexpr int U = 4;
+  const int CV = C / 8;  // a power of two (host-checked): the grid stride keeps the thread's channels
   const int cv_shift = __ffs(CV) - 1;
+  // 32-bit vector indices (the host checks nvec < 2^31)
+  const uint32_t n = (uint32_t)nvec;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = (int)(i0 & (CV - 1)) * 8;
+  const uint4* __restrict__ xg = reinterpret_cast<const uint4*>(x);
+  const uint4* __restrict__ dg = reinterpret_cast<const uint4*>(src.dy);
+  const uint4* __restrict__ ag = reinterpret_cast<const uint4*>(add);
+  uint4* __restrict__ og = reinterpret_cast<uint4*>(dx);
+  const uint32_t safe = i0 < n ? i0 : 0;
+  uint4 xr[U], dr[U], ar[U];
+  auto load = [&](uint32_t base) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = base + u * stride < n ? base + u * stride : safe;  // clamped: the store is skipped
+      xr[u] = xg[i];
+      if constexpr (!POOL) dr[u] = dg[i];
+      if constexpr (ADD) ar[u] = ag[i];
+    }
+  };
+  load(i0);
   float sc[8], sh[8], A[8], B[8], D[8];
-  {
+  load8f(scale + c, sc);
+  load8f(shift + c, sh);
+  if constexpr (FIN) {
+    const bool pub = f.publish && blockIdx.x == 0;
+    for (int cc = threadIdx.x; cc < C; cc += blockDim.x) drn_bn_fin_bwd(f, cc, pub, lsm[cc], lsm[C + cc], lsm[2 * C + cc]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      A[j] = lsm[c + j];
+      B[j] = lsm[C + c + j];
+      D[j] = lsm[2 * C + c + j];
+    }
+  } else {
+    // the affine form dx = A*g + B*x + D folds k1*(g - k2 - (x-mu)*is*k3)
     float mu[8], is[8], k1[8], k2[8], k3[8];
-    load8f(scale + c, sc);
-    load8f(shift + c, sh);
     load8f(mean + c, mu);
     load8f(invstd + c, is);
     load8f(coef + c, k1);
@@ -414,32 +448,34 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(DySrc src, const bf16
       D[j] = -k1[j] * k2[j] + k1[j] * k3[j] * is[j] * mu[j];
     }
   }
-  // two vectors in flight per thread, as the finalizing variant below
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const uint4* xv = reinterpret_cast<const uint4*>(x);
-  const uint4* av = reinterpret_cast<const uint4*>(add);
-  uint4* dv = reinterpret_cast<uint4*>(dx);
-  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-  int64_t i = i0;
-  for (; i + stride < nvec; i += 2 * stride) {
-    float fd0[8], fd1[8];
-    const uint4 x0 = xv[i], x1 = xv[i + stride];
-    const uint4 a0 = ADD ? av[i] : z, a1 = ADD ? av[i + stride] : z;
-    src.load_vec(i, cv_shift, C, c, fd0);
-    src.load_vec(i + stride, cv_shift, C, c, fd1);
-    bn_bwd_fin_vec<ADD>(x0, fd0, a0, A, B, D, sc, sh, relu);
-    bn_bwd_fin_vec<ADD>(x1, fd1, a1, A, B, D, sc, sh, relu);
-    dv[i] = pack8(fd0);
-    dv[i + stride] = pack8(fd1);
+  for (uint32_t base = i0; base < n; base += U * stride) {
+    uint4 o[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float fd[8];
+      if constexpr (POOL) src.load_vec(base + u * stride < n ? base + u * stride : safe, cv_shift, C, c, fd);
+      else unpack8(dr[u], fd);
+      bn_bwd_fin_vec<ADD>(xr[u], fd, ar[u], A, B, D, sc, sh, relu);
+      o[u] = pack8(fd);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (base + u * stride < n) og[base + u * stride] = o[u];
+    if (base + U * stride < n) load(base + U * stride);
   }
-  if (i < nvec) {
-    float fd0[8];
-    const uint4 x0 = xv[i];
-    const uint4 a0 = ADD ? av[i] : z;
-    src.load_vec(i, cv_shift, C, c, fd0);
-    bn_bwd_fin_vec<ADD>(x0, fd0, a0, A, B, D, sc, sh, relu);
-    dv[i] = pack8(fd0);
-  }
+}
+
+template <bool ADD, bool POOL>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(DySrc src, const bf16_t* __restrict__ x,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ invstd,
+                                                           const float* __restrict__ coef,
+                                                           const bf16_t* __restrict__ add, bf16_t* __restrict__ dx,
+                                                           int64_t nvec, int C, int relu) {
+  DrnBnFin f{};
+  bn_bwd_apply_body<ADD, false, POOL>(src, x, scale, shift, mean, invstd, coef, f, add, dx, nvec, C, relu, nullptr);
 }
 
 // bn_finalize_bwd fused into the apply: coefficients per thread from the [2][C] sums (sum g,
@@ -557,80 +593,21 @@ __global__ __launch_bounds__(256) void bn_apply_fin_kernel(const bf16_t* __restr
 // (relu=0: the producing data-gradient conv masked it in its epilogue); A/B/D of every channel
 // finalized in the prologue from the backward sums, workgroup 0 of a publishing launch writes
 // dgamma/dbeta. scale/shift (for the mask) and mean/invstd are the forward's published values.
-template <bool ADD>
+template <bool ADD, bool POOL>
 __global__ __launch_bounds__(256) void bn_bwd_apply_fin_kernel(DySrc src, const bf16_t* __restrict__ x,
                                                                const float* __restrict__ scale,
                                                                const float* __restrict__ shift, DrnBnFin f,
                                                                const bf16_t* __restrict__ add, bf16_t* __restrict__ dx,
                                                                int64_t nvec, int C, int relu) {
   extern __shared__ __attribute__((aligned(16))) float lsm[];  // [3][C]
-  const bool pub = f.publish && blockIdx.x == 0;
-  for (int c = threadIdx.x; c < C; c += 256) drn_bn_fin_bwd(f, c, pub, lsm[c], lsm[C + c], lsm[2 * C + c]);
-  __syncthreads();
-  const int CV = C / 8;
-  const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int c = (int)(i0 & (CV - 1)) * 8;
-  const int cv_shift = __ffs(CV) - 1;
-  float A[8], B[8], D[8], sc[8], sh[8];
-  load8f(scale + c, sc);
-  load8f(shift + c, sh);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    A[j] = lsm[c + j];
-    B[j] = lsm[C + c + j];
-    D[j] = lsm[2 * C + c + j];
-  }
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const uint4* xv = reinterpret_cast<const uint4*>(x);
-  const uint4* av = reinterpret_cast<const uint4*>(add);
-  uint4* dv = reinterpret_cast<uint4*>(dx);
-  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-  int64_t i = i0;
-  for (; i + stride < nvec; i += 2 * stride) {
-    float fd0[8], fd1[8];
-    const uint4 x0 = xv[i], x1 = xv[i + stride];
-    const uint4 a0 = ADD ? av[i] : z, a1 = ADD ? av[i + stride] : z;
-    src.load_vec(i, cv_shift, C, c, fd0);
-    src.load_vec(i + stride, cv_shift, C, c, fd1);
-    bn_bwd_fin_vec<ADD>(x0, fd0, a0, A, B, D, sc, sh, relu);
-    bn_bwd_fin_vec<ADD>(x1, fd1, a1, A, B, D, sc, sh, relu);
-    dv[i] = pack8(fd0);
-    dv[i + stride] = pack8(fd1);
-  }
-  if (i < nvec) {
-    float fd0[8];
-    const uint4 x0 = xv[i];
-    const uint4 a0 = ADD ? av[i] : z;
-    src.load_vec(i, cv_shift, C, c, fd0);
-    bn_bwd_fin_vec<ADD>(x0, fd0, a0, A, B, D, sc, sh, relu);
-    dv[i] = pack8(fd0);
-  }
+  bn_bwd_apply_body<ADD, true, POOL>(src, x, scale, shift, nullptr, nullptr, nullptr, f, add, dx, nvec, C, relu, lsm);
 }
 
-// grid of the finalizing apply kernels: every workgroup re-derives the parameters of all C
-// channels (2*G*C + ~4*C floats from L2), so the grid is capped lower than the plain apply's
-static inline int grid_for_fin(int64_t nvec) {
-  static int cap = 0;
-  if (cap == 0) {
-    const char* e = getenv("DRN_BN_FIN_GRID");
-    cap = e ? atoi(e) : 2048;
-    if (cap < 1) cap = 2048;
-  }
-  int64_t b = (nvec + 511) / 512;  // >= 2 vectors per thread
+// grid of the streaming kernels: one workgroup per 256 vectors (per 1024 for the backward applies'
+// 4-vector batches), at most 2048 = 8 per CU (measured: 2048 < 4096 < 8192 < 16384 workgroups)
+static inline int grid_for(int64_t nvec, int per_thread = 1, int cap = 2048) {
+  int64_t b = (nvec + 256 * per_thread - 1) / (256 * per_thread);
   if (b > cap) b = cap;
-  if (b < 1) b = 1;
-  return (int)b;
-}
-
-static int g_apply_grid_cap = 0;
-static inline int grid_for(int64_t nvec) {
-  if (g_apply_grid_cap == 0) {
-    const char* e = getenv("DRN_BN_APPLY_GRID");
-    g_apply_grid_cap = e ? atoi(e) : 2048;  // measured: 2048 < 4096 < 8192 < 16384 workgroups
-    if (g_apply_grid_cap < 1) g_apply_grid_cap = 8192;
-  }
-  int64_t b = (nvec + 255) / 256;
-  if (b > g_apply_grid_cap) b = g_apply_grid_cap;
   if (b < 1) b = 1;
   return (int)b;
 }
@@ -735,7 +712,7 @@ DRN_API int drn_bn_apply_fin(const void* x, void* y, const DrnBnFin* f, int64_t 
       (f->publish && (f->scale == nullptr || f->shift == nullptr || f->mean == nullptr || f->invstd == nullptr)))
     return (int)hipErrorInvalidValue;
   const int64_t nvec = M * (C / 8);
-  hipLaunchKernelGGL(drn::bn_apply_fin_kernel, dim3(drn::grid_for_fin(nvec)), dim3(256), 2 * C * sizeof(float), s,
+  hipLaunchKernelGGL(drn::bn_apply_fin_kernel, dim3(drn::grid_for(nvec, 2)), dim3(256), 2 * C * sizeof(float), s,
                      (const bf16_t*)x, (bf16_t*)y, *f, nvec, C / 8, relu);
   return (int)hipGetLastError();
 }
@@ -747,15 +724,21 @@ DRN_API int drn_bn_bwd_apply_fin(const void* dy, const float* dpool, int pool_hw
       (f->publish && (f->dgamma == nullptr || f->dbeta == nullptr)))
     return (int)hipErrorInvalidValue;
   const int64_t nvec = M * (C / 8);
+  if (nvec >= (int64_t(1) << 31)) return (int)hipErrorInvalidValue;  // 32-bit vector indices
   drn::DySrc src{(const bf16_t*)dy, dpool, pool_hw};
-  if (add != nullptr)
-    hipLaunchKernelGGL(drn::bn_bwd_apply_fin_kernel<true>, dim3(drn::grid_for_fin(nvec)), dim3(256),
-                       3 * C * sizeof(float), s, src, (const bf16_t*)x, scale, shift, *f, (const bf16_t*)add,
-                       (bf16_t*)dx, nvec, C, relu);
-  else
-    hipLaunchKernelGGL(drn::bn_bwd_apply_fin_kernel<false>, dim3(drn::grid_for_fin(nvec)), dim3(256),
-                       3 * C * sizeof(float), s, src, (const bf16_t*)x, scale, shift, *f, (const bf16_t*)add,
-                       (bf16_t*)dx, nvec, C, relu);
+  const dim3 grid(drn::grid_for(nvec, 4, 1024));  // 4 workgroups per CU (<= 128 VGPRs)
+  const size_t lds = 3 * C * sizeof(float);
+#define DRN_BWD_FIN(ADD, POOL)                                                                                     \
+  hipLaunchKernelGGL((drn::bn_bwd_apply_fin_kernel<ADD, POOL>), grid, dim3(256), lds, s, src, (const bf16_t*)x, scale, \
+                     shift, *f, (const bf16_t*)add, (bf16_t*)dx, nvec, C, relu)
+  if (pool_hw > 0) {
+    if (add != nullptr) DRN_BWD_FIN(true, true);
+    else DRN_BWD_FIN(false, true);
+  } else {
+    if (add != nullptr) DRN_BWD_FIN(true, false);
+    else DRN_BWD_FIN(false, false);
+  }
+#undef DRN_BWD_FIN
   return (int)hipGetLastError();
 }
 
@@ -768,14 +751,19 @@ DRN_API int drn_bn_bwd_apply(const void* dy, const float* dpool, int pool_hw, co
                              const void* add, void* dx, int64_t M, int C, int relu, hipStream_t s) {
   if (C % 8 || !pow2(C / 8) || C / 8 > 256) return (int)hipErrorInvalidValue;
   const int64_t nvec = M * (C / 8);
+  if (nvec >= (int64_t(1) << 31)) return (int)hipErrorInvalidValue;  // 32-bit vector indices
   drn::DySrc src{(const bf16_t*)dy, dpool, pool_hw};
-  if (add != nullptr)
-    hipLaunchKernelGGL(drn::bn_bwd_apply_kernel<true>, dim3(drn::grid_for(nvec)), dim3(256), 0, s, src,
-                       (const bf16_t*)x, scale, shift, mean, invstd, coef, (const bf16_t*)add, (bf16_t*)dx, nvec, C,
-                       relu);
-  else
-    hipLaunchKernelGGL(drn::bn_bwd_apply_kernel<false>, dim3(drn::grid_for(nvec)), dim3(256), 0, s, src,
-                       (const bf16_t*)x, scale, shift, mean, invstd, coef, (const bf16_t*)add, (bf16_t*)dx, nvec, C,
-                       relu);
+  const dim3 grid(drn::grid_for(nvec, 4, 1024));  // 4 workgroups per CU (<= 128 VGPRs)
+#define DRN_BWD(ADD, POOL)                                                                                         \
+  hipLaunchKernelGGL((drn::bn_bwd_apply_kernel<ADD, POOL>), grid, dim3(256), 0, s, src, (const bf16_t*)x, scale, shift, \
+                     mean, invstd, coef, (const bf16_t*)add, (bf16_t*)dx, nvec, C, relu)
+  if (pool_hw > 0) {
+    if (add != nullptr) DRN_BWD(true, true);
+    else DRN_BWD(false, true);
+  } else {
+    if (add != nullptr) DRN_BWD(true, false);
+    else DRN_BWD(false, false);
+  }
+#undef DRN_BWD
   return (int)hipGetLastError();
 }

@@ -1359,11 +1359,6 @@ DRN_API int drn_conv_fwd_tiles_p(int M, int K) {
 DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s);
 
 #define DRN_GLDS_NCFG 38
-// halo-tiled direct 3x3 family (conv_halo.hip): configuration ids DRN_HALO_CFG0 + i
-#define DRN_HALO_CFG0 300
-DRN_API int drn_conv_halo(int cfg, const DrnConvFwdArgs* a, const void* zero, hipStream_t s);
-DRN_API int drn_conv_halo_ok(const DrnConvFwdArgs* a);
-DRN_API int drn_conv_halo_cfg0() { return DRN_HALO_CFG0; }
 
 // Whether the LDS-DMA kernel family supports this convolution.
 DRN_API int drn_conv_glds_ok(const DrnConvFwdArgs* a) {
@@ -1393,7 +1388,6 @@ DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
       (a->cfg < 0 || a->cfg >= DRN_GLDS_NCFG || !drn_conv_glds_ok(a) || zero == nullptr))
     return (int)hipErrorInvalidValue;  // split-K: explicit split-capable LDS-DMA configurations only
   if (a->cfg >= DRN_NK_CFG0 && a->cfg < DRN_NK_CFG0 + DRN_NK_NCFG) return drn::launch_conv_nk(a->cfg - DRN_NK_CFG0, a, s);
-  if (a->cfg >= DRN_HALO_CFG0 && a->cfg < DRN_HALO_CFG0 + 100) return drn_conv_halo(a->cfg - DRN_HALO_CFG0, a, zero, s);
   if (a->cfg >= DRN_GLDS_NCFG && a->cfg != 100) return (int)hipErrorInvalidValue;
   if (a->bnb_x != nullptr && (!drn_conv_glds_ok(a) || zero == nullptr || a->cfg == 100))
     return (int)hipErrorInvalidValue;  // the BN-backward input transform exists on the LDS-DMA path only

@@ -129,10 +129,6 @@ _SIGS = {
     "drn_conv_sk_slots_cfg": ([c_p, c_int, c_int], c_int),
     "drn_conv_nk_num_cfgs": ([], c_int),
     "drn_conv_nk_cfg0": ([], c_int),
-    "drn_conv_halo_ok": ([ctypes.POINTER(DrnConvFwdArgs)], c_int),
-    "drn_conv_halo_num_cfgs": ([], c_int),
-    "drn_conv_halo_cfg0": ([], c_int),
-    "drn_conv_halo": ([c_int, ctypes.POINTER(DrnConvFwdArgs), c_p, c_p], c_int),
     "drn_p2p_alloc": ([ctypes.POINTER(c_p), ctypes.c_size_t], c_int),
     "drn_p2p_free": ([c_p], c_int),
     "drn_bn_fin_size": ([], c_int),

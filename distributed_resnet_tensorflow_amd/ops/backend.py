@@ -407,8 +407,7 @@ class HipBackend(_Common):
         per distinct convolution before the step is captured) and return the fastest. Runs on
         scratch outputs / statistics so no live buffer is modified. Every configuration
         accumulates each output in the same k order, so the choice does not change numerics."""
-        halo = bool(self.L.drn_conv_halo_ok(ctypes.byref(a)))
-        if not self.L.drn_conv_glds_ok(ctypes.byref(a)) and not halo:
+        if not self.L.drn_conv_glds_ok(ctypes.byref(a)):
             return (100, 1)
         iters = iters or self.tune_iters
         N, K = a.N, a.K
@@ -430,12 +429,10 @@ class HipBackend(_Common):
         cands = os.environ.get("DRN_CONV_CANDS")
         if cands:
             cands = [int(c) for c in cands.split(",")]
-        else:  # register-staged, LDS-DMA, narrow-output (K = 16 / 32), halo-tiled 3x3 configurations
+        else:  # register-staged, LDS-DMA and narrow-output (K = 16 / 32) configurations
             nk0 = self.L.drn_conv_nk_cfg0()
-            h0 = self.L.drn_conv_halo_cfg0()
             cands = [100] + list(range(self.L.drn_conv_glds_num_cfgs())) + \
-                [nk0 + i for i in range(self.L.drn_conv_nk_num_cfgs())] * (a.K in (16, 32)) + \
-                [h0 + i for i in range(self.L.drn_conv_halo_num_cfgs())] * halo
+                [nk0 + i for i in range(self.L.drn_conv_nk_num_cfgs())] * (a.K in (16, 32))
 
         def setk(c):
             t.cfg, ks = c

@@ -58,7 +58,7 @@ def source_hash(kernels: Path = KERNELS, include: Path = INCLUDE) -> str:
 
 # kernels whose code the tuner's choices depend on (the conv / weight-gradient / stem tiles and
 # their fused prologues / epilogues, all through the shared headers)
-TUNE_SOURCES = ("conv_fwd.hip", "conv_halo.hip", "conv_wgrad.hip", "stem.hip")
+TUNE_SOURCES = ("conv_fwd.hip", "conv_wgrad.hip", "stem.hip")
 
 
 def tune_hash(kernels: Path = KERNELS, include: Path = INCLUDE) -> str:

@@ -177,17 +177,11 @@ class Executor:
         # per consuming tile, and the streaming pass it replaces is pure HBM traffic -- and
         # materialise BNs feeding a 3x3 conv, whose 9 taps would transform every element 9 times.
         # "all" materialises every BN, "none" fuses every BN (DRN_BN_MATERIALIZE).
-        # "halo": as "1x1", but BNs feeding a stride-1 3x3 conv are fused too (the halo-tiled
-        # kernel, conv_halo.hip, transforms each staged input element once per tile instead of
-        # once per tap). Measured slower than materialising (ResNet-50 bs128, one box, 2 rounds:
-        # 12,926-12,930 vs 13,097-13,102 img/s, profiles/r4_experiments.md): kept as an option.
         if materialize_bn is None:
             policy = os.environ.get("DRN_BN_MATERIALIZE", "1x1" if self.is_hip else "all")
-            if os.environ.get("DRN_FUSE_BN_PROLOGUE") == "1":
-                policy = "none"
         else:
             policy = "all" if materialize_bn else "none"
-        assert policy in ("all", "1x1", "halo", "none"), policy
+        assert policy in ("all", "1x1", "none"), policy
         self.bn_policy = policy
         self.materialize_bn = policy != "none"
         # ... and (policy "1x1") BNs whose 1x1 consumer has >= DRN_BN_MAT_TILES 128-wide output-
@@ -432,9 +426,8 @@ class Executor:
                 big = b.src.numel() >= self.mat_min_elems
 
                 def fusable(c):
-                    halo = self.bn_policy == "halo" and c.k == 3 and c.stride == 1 and c.cin_store % 64 == 0
-                    return (c.k == 1 or halo) and -(-c.cout // 128) < self.mat_tiles
-                if self.bn_policy == "all" or (self.bn_policy in ("1x1", "halo") and big and
+                    return c.k == 1 and -(-c.cout // 128) < self.mat_tiles
+                if self.bn_policy == "all" or (self.bn_policy == "1x1" and big and
                                                not all(fusable(c) for c in consumers)):
                     b.act = self._act(*b.src.shape)
         for b in [b for bp in self.blocks for b in bp.bn] + [self.final_bn]:

@@ -873,6 +873,42 @@ def test_bn_bwd_apply_fin_non_publishing(hip, C):
     assert not bool((res[True][1] == 7.0).all())
 
 
+@pytest.mark.parametrize("M,C", [(100352, 128), (25088 + 7, 256), (391, 2048)])
+@pytest.mark.parametrize("fin", [True, False])
+@pytest.mark.parametrize("add", [False, True])
+def test_bn_bwd_apply_batches(hip, M, C, fin, add):
+    """The backward applies' 4-vector batches (loads issued before the coefficient prologue, the
+    last batch partial, clamped loads past the end) on tensors of several batches per thread,
+    against the affine form dx = A*g + B*x + D (+ add) computed in fp32 by PyTorch."""
+    from distributed_resnet_tensorflow_amd.ops.backend import BnCfin
+    torch.manual_seed(21)
+    x = bf(torch.randn(M, C) * 1.5 + 0.2).cuda()
+    dy = bf(torch.randn(M, C)).cuda()
+    a = bf(torch.randn(M, C)).cuda() if add else None
+    sc, sh = (torch.rand(C) + 0.5).cuda(), (torch.randn(C) * 0.3).cuda()
+    mu, isd = (torch.randn(C) * 0.1).cuda(), (torch.rand(C) + 0.5).cuda()
+    gamma = (torch.rand(C) + 0.5).cuda()
+    bst = (torch.randn(3, 2, C) * M ** 0.5).cuda()
+    sg, sgx = bst[:, 0].sum(0), bst[:, 1].sum(0)
+    k1, k2, k3 = gamma * isd, sg / M, sgx / M
+    dx = torch.full_like(x, float("nan"))
+    if fin:
+        dg, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+        hip.bn_bwd_apply_fin(dy, None, 0, x, sc, sh, BnCfin(bst, float(M), gamma, mean=mu, invstd=isd, dgamma=dg,
+                                                           dbeta=db, publish=True), a, dx, relu=True)
+        assert rel(dg, sgx) < 1e-5 and rel(db, sg) < 1e-5
+    else:
+        coef = torch.cat([k1, k2, k3])
+        hip.bn_bwd_apply(dy, None, 0, x, sc, sh, mu, isd, coef, a, dx, relu=True)
+    xf = x.float()
+    g = dy.float() * ((xf * sc + sh) > 0).float()
+    want = k1 * (g - k2 - (xf - mu) * isd * k3)
+    if add:
+        want = want + a.float()
+    assert bool(torch.isfinite(dx.float()).all())   # every element written (the tail included)
+    assert rel(dx.float(), want) < 1e-2
+
+
 @pytest.mark.parametrize("publish", [True, False])
 @pytest.mark.parametrize("nk", [False, True])
 def test_conv_prologue_finalize(hip, ref, publish, nk):
