@@ -74,7 +74,7 @@ def main():
     # measure the DP step machinery on one GPU
     force_dp = os.environ.get("DRN_BENCH_DP") == "1"
     if force_dp and world == 1 and "MASTER_ADDR" not in os.environ:
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("DRN_BENCH_PORT", "29533"),
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29533"),
                           RANK="0", WORLD_SIZE="1")
     from distributed_resnet_tensorflow_amd.models.spec import build_spec
     spec = build_spec(args.dataset, args.resnet_size, width=args.width)

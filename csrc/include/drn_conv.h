@@ -179,12 +179,6 @@ struct DrnConvFwdArgs {
   // prologue): when in_fin.stats is set the prologue derives scale/shift from the statistics
   // instead of reading in_scale/in_shift (see DrnBnFin).
   DrnBnFin in_fin;
-  // Optional fused BatchNorm-backward input (data gradients, LDS-DMA kernels): the conv input
-  // dY is dx of a BatchNorm whose apply was not materialised, dY = A*x + B*bnb_x + D per
-  // channel with (A, B, D) finalized from bnb_fin's backward statistics (drn_bn_fin_bwd);
-  // x holds the ReLU-masked gradient g, bnb_x the BatchNorm's input.
-  const void* bnb_x;
-  DrnBnFin bnb_fin;
   // Split-K (LDS-DMA kernels, ksplit > 1): partial-tile workspace [tiles][ksplit][BP*BC] fp32 and
   // one zeroed ticket word per output tile (the last arriver re-arms it).
   // Stream-K (sk_blocks > 0): sk_blocks workgroups share the tiles x k-stages units evenly;
@@ -209,9 +203,6 @@ struct DrnConvWgradArgs {
   int32_t relu_in;
   int32_t splits, pix_per_split;
   DrnFastDiv fd_pq, fd_q;
-  // Optional fused BatchNorm-backward dY (see DrnConvFwdArgs::bnb_x): dY_eff = A*dy + B*bnb_x + D
-  const void* bnb_x;
-  DrnBnFin bnb_fin;
   // 1: every split adds its tile into out = the final, pre-zeroed gradient with fp32 atomics
   // (no partial slabs, no drn_splitk_reduce)
   int32_t atomic_out;

@@ -209,12 +209,12 @@ __device__ __forceinline__ void conv_epilogue_pass(const DrnConvFwdArgs& a, char
   const bool has_res = a.residual != nullptr;
   const int ch = tid % CHR;
   const int c = c0 + ch * 8;
-  const bool bnb = a.bn_x != nullptr;
+  const bool bwd = a.bn_x != nullptr;
   float ssum[8], ssq[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) ssum[j] = ssq[j] = 0.f;
   float bsc[8], bsh[8], bmu[8], bis[8];
-  if (bnb && c < a.K) {
+  if (bwd && c < a.K) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       bsc[j] = a.bn_scale[c + j];
@@ -241,7 +241,7 @@ __device__ __forceinline__ void conv_epilogue_pass(const DrnConvFwdArgs& a, char
       const uint4 o = pack8(f);
       float q8[8];
       unpack8(o, q8);
-      if (bnb) {
+      if (bwd) {
         // BN-backward: mask by the forward ReLU, accumulate sum g and sum g * xhat
         float xb[8];
         if constexpr (PF) unpack8(e.bx[it], xb);

@@ -261,12 +261,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(DrnConvFwdArgs a) {
 // bank-conflict free (checked exhaustively against the gfx950 lane-group table).
 // ---------------------------------------------------------------------------------------
 // Order of the k-stages (tap r, tap s, channel chunk ci) of the LDS-DMA kernels: taps outer,
-// channel chunks inner (KRSC order). -DDRN_KORDER_CHUNK_OUTER fetches the R*S shifted windows
-// of one channel chunk in consecutive stages instead (shorter L2 reuse distance); measured
-// identical on every ResNet-50 3x3 layer and on the step (profiles/r2_experiments.md).
+// channel chunks inner (KRSC order; the chunk-outer order measured identical, profiles/r2_experiments.md).
 template <int BK>
 __device__ __forceinline__ void kstep_next(int& r, int& s, int& ci, int R, int S, int C) {
-#ifndef DRN_KORDER_CHUNK_OUTER
   if ((ci += BK) == C) {
     ci = 0;
     if (++s == S) {
@@ -274,15 +271,6 @@ __device__ __forceinline__ void kstep_next(int& r, int& s, int& ci, int R, int S
       ++r;
     }
   }
-#else
-  if (++s == S) {
-    s = 0;
-    if (++r == R) {
-      r = 0;
-      ci += BK;
-    }
-  }
-#endif
 }
 
 // PRO: the input is the RAW pre-BN tensor and the kernel applies relu(x * in_scale + in_shift)
@@ -301,15 +289,6 @@ __device__ __forceinline__ void kstep_next(int& r, int& s, int& ci, int R, int S
 // 64/(S*C) of the work instead of falling back to the register-staged kernel. With PRO the
 // fused BN prologue uses the lane's fixed chunk channel offset.
 //
-// BNB: the input dY of this (data-gradient) convolution is the output of a BatchNorm backward
-// that is NOT materialised: dY = A[c] * g + B[c] * x + D[c] (dx = gamma*invstd * (g - mean g -
-// xhat * mean(g*xhat)) folded per channel, drn_bn_fin_bwd), with g = a.x the ReLU-masked
-// gradient and x = a.bnb_x the BatchNorm's input. Each stage DMAs the x pieces next to the g
-// pieces ([A rows][B rows][X rows]); after the counted vmcnt wait every lane rewrites its own
-// landed g pieces in place (the same one-LDS-round-trip scheme as PRO), zero pieces stay zero.
-// The coefficients come from the BN statistics replicas in the prologue (consumer-side
-// finalize; the first workgroup of the publishing launch writes dgamma / dbeta).
-//
 // KS (split-K, a.ksplit = S > 1): the grid is tiles x S; workgroup (tile, s) runs k-stages
 // [s*T/S, (s+1)*T/S) of its tile, stores its fp32 partial accumulators to a.ks_ws and takes a
 // ticket; the LAST arriver of a tile sums the S partials in split order (fixed order: bitwise
@@ -318,13 +297,12 @@ __device__ __forceinline__ void kstep_next(int& r, int& s, int& ci, int R, int S
 // pair of the CDNA4 guide (G16). For under-filled grids (e.g. 196 tiles of a 7x7-stage 3x3
 // conv on 256 CUs) it trades 64 KB of partial traffic per extra split for a full chip.
 template <int BP, int BC, int WAVES_P, int NS, int NW = 4, bool PF = true, int BK = 64, bool PRO = false,
-          bool SROW = false, bool BNB = false, int NH = 1, bool KS = false, bool IL = false>
+          bool SROW = false, int NH = 1, bool KS = false, bool IL = false>
 __device__ __forceinline__ void conv_fwd_glds_tile(const DrnConvFwdArgs& a, const void* __restrict__ zero, char* smem,
                                                    int bid, int ksn, int ksi, int ks_stride, int t_beg_in,
                                                    int t_cnt_in) {
   static_assert(BK == 64 || BK == 32, "k per stage");
   static_assert(!SROW || BK == 64, "row-staged narrow convs: 64-deep stages");
-  static_assert(!(BNB && (PRO || SROW)), "one input transform per launch");
   constexpr int NT = NW * 64;
   constexpr int WAVES_C = NW / WAVES_P;
   constexpr int WP = BP / WAVES_P, WC = BC / WAVES_C;
@@ -332,14 +310,14 @@ __device__ __forceinline__ void conv_fwd_glds_tile(const DrnConvFwdArgs& a, cons
   constexpr int ROWB = BK * 2;              // bytes of one LDS row (BK bf16 of k)
   constexpr int CPR = BK / 8;               // 16-byte chunks per row
   constexpr int RPG = 1024 / ROWB;          // rows per glds wave-instruction (1 KiB)
-  constexpr int STAGE = (BC + BP * (BNB ? 2 : 1)) * ROWB;
+  constexpr int STAGE = (BC + BP) * ROWB;
   constexpr int GA = BC / (RPG * NW), GB = BP / (RPG * NW);  // glds wave-instructions per stage
-  constexpr int G = GA + GB * (BNB ? 2 : 1);
+  constexpr int G = GA + GB;
   constexpr int D = NS - 1;                 // stages in flight ahead of the computing one
   static_assert(WAVES_P * WAVES_C == NW && MI >= 1 && MJ >= 1, "wave layout");
   static_assert(GA * RPG * NW == BC && GB * RPG * NW == BP, "rows must split evenly over the waves");
   static_assert(NS >= 2 && G * (D > 1 ? D - 1 : 1) < 64, "pipeline depth");
-  static_assert(NH == 1 || (!PF && !SROW && !BNB), "sliced epilogue: big-tile plain / PRO kernels only");
+  static_assert(NH == 1 || (!PF && !SROW), "sliced epilogue: big-tile plain / PRO kernels only");
 
 #ifdef DRN_CONV_TRACE
   unsigned long long* const trace = g_conv_trace;
@@ -353,7 +331,7 @@ __device__ __forceinline__ void conv_fwd_glds_tile(const DrnConvFwdArgs& a, cons
   const int C = a.C;
   const int Ktot = a.R * a.S * C;
   const int ntc = (a.K + BC - 1) / BC;
-  static_assert(!KS || (!SROW && !BNB), "split-K: plain / fused-BN-prologue inputs");
+  static_assert(!KS || !SROW, "split-K: plain / fused-BN-prologue inputs");
   const int tc = bid % ntc;
   const int tp = bid / ntc;
   const int m0 = tp * BP;
@@ -400,12 +378,8 @@ __device__ __forceinline__ void conv_fwd_glds_tile(const DrnConvFwdArgs& a, cons
   // wholly inside the output is a valid pixel for the whole reduction, and with a full channel
   // tile every A row is a real filter -- such stages issue each piece as a wave-uniform stage base
   // plus a per-lane offset fixed for the whole kernel, with no per-lane test.
-#ifndef DRN_NO_FAST_LOADER  // (-DDRN_NO_FAST_LOADER: the per-lane path everywhere, for A/B variant builds)
-  const bool fast_b = !SROW && !BNB && a.R == 1 && a.S == 1 && a.pad_h == 0 && a.pad_w == 0 && m0 + BP <= M;
+  const bool fast_b = !SROW && a.R == 1 && a.S == 1 && a.pad_h == 0 && a.pad_w == 0 && m0 + BP <= M;
   const bool fast_a = !SROW && c0 + BC <= a.K;
-#else
-  const bool fast_b = false, fast_a = false;
-#endif
   uint32_t aoff_w[GA], boff_x[GB];
 #pragma unroll
   for (int i = 0; i < GA; ++i)
@@ -476,21 +450,11 @@ __device__ __forceinline__ void conv_fwd_glds_tile(const DrnConvFwdArgs& a, cons
         glds16(src, st + (BC + RPG * NW * i + RPG * wave) * ROWB);
       }
     }
-    if constexpr (BNB) {  // the BatchNorm input pieces at the same positions
-      const bf16_t* __restrict__ bx = reinterpret_cast<const bf16_t*>(a.bnb_x);
-#pragma unroll
-      for (int i = 0; i < GB; ++i) {
-        const int h = bh[i] + ir, w = bw[i] + is;
-        const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-        const void* src = ok ? (const void*)(bx + (boff[i] + tap_off)) : zero;
-        glds16(src, st + (BC + BP + RPG * NW * i + RPG * wave) * ROWB);
-      }
-    }
     kstep_next<BK>(ir, is, ici, a.R, a.S, C);
     ik = (ir * a.S + is) * C + ici;
   };
-  // IL: the same stage issued one LDS-DMA piece at a time (g = 0 .. G-1, A pieces then B pieces
-  // then BNB pieces), interleaved with the MFMAs of the computing stage by the main loop; then
+  // IL: the same stage issued one LDS-DMA piece at a time (g = 0 .. G-1, A pieces then B pieces),
+  // interleaved with the MFMAs of the computing stage by the main loop; then
   // issue_advance() moves the k iterator
   auto issue_piece = [&](int slot, int g) {
     char* st = smem + slot * STAGE;
@@ -499,16 +463,11 @@ __device__ __forceinline__ void conv_fwd_glds_tile(const DrnConvFwdArgs& a, cons
       glds16(src, st + (RPG * NW * g + RPG * wave) * ROWB);
       return;
     }
-    const int i = (g - GA) % GB;
+    const int i = g - GA;
     const int h = bh[i] + ir, w = bw[i] + is;
     const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
     const int off = boff[i] + (ir * a.W + is) * C + ici;
-    if (g < GA + GB) {
-      glds16(ok ? (const void*)(xg + off) : zero, st + (BC + RPG * NW * i + RPG * wave) * ROWB);
-    } else if constexpr (BNB) {
-      const bf16_t* __restrict__ bx = reinterpret_cast<const bf16_t*>(a.bnb_x);
-      glds16(ok ? (const void*)(bx + off) : zero, st + (BC + BP + RPG * NW * i + RPG * wave) * ROWB);
-    }
+    glds16(ok ? (const void*)(xg + off) : zero, st + (BC + RPG * NW * i + RPG * wave) * ROWB);
   };
   auto issue_advance = [&]() {
     kstep_next<BK>(ir, is, ici, a.R, a.S, C);
@@ -568,61 +527,10 @@ __device__ __forceinline__ void conv_fwd_glds_tile(const DrnConvFwdArgs& a, cons
     }
     __syncthreads();
   }
-  if constexpr (BNB) {
-    // consumer-side BN-backward finalize: dY = A*g + B*x + D per channel, [A C][B C][D C]
-    const bool pub = a.bnb_fin.publish && blockIdx.x == 0;
-    for (int c = tid; c < C; c += NT) drn_bn_fin_bwd(a.bnb_fin, c, pub, ssl[c], ssl[C + c], ssl[2 * C + c]);
-    __syncthreads();
-  }
-
   for (int t = 0; t < T; ++t) {
     // retire stage t: the stages issued after it (up to D-1) may stay in flight
     if (t + D - 1 < T) wait_vmcnt<G * (D - 1)>();
     else wait_vmcnt<0>();
-    if constexpr (BNB) {
-      char* sw = smem + (t % NS) * STAGE;
-      const uint32_t sp = lds_addr(ssl + xci + lcb * 8);
-      u32x4_t v[2 * GB + 6];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        v[2 * GB + 2 * q] = lds_read16(sp + 4 * q * C);
-        v[2 * GB + 2 * q + 1] = lds_read16(sp + 4 * q * C + 16);
-      }
-      uint32_t pa[GB], ok = 0;
-#pragma unroll
-      for (int i = 0; i < GB; ++i) {
-        const int h = bh[i] + xr, w = bw[i] + xs;
-        ok |= ((unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W) ? (1u << i) : 0u;
-        pa[i] = lds_addr(sw + (BC + RPG * NW * i + RPG * wave) * ROWB + lane * 16);
-        v[i] = lds_read16(pa[i]);
-        v[GB + i] = lds_read16(pa[i] + BP * ROWB);
-      }
-      lds_wait_all<2 * GB + 6>(v);
-      float cA[8], cB[8], cD[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        cA[e] = __uint_as_float(v[2 * GB + (e >> 2)][e & 3]);
-        cB[e] = __uint_as_float(v[2 * GB + 2 + (e >> 2)][e & 3]);
-        cD[e] = __uint_as_float(v[2 * GB + 4 + (e >> 2)][e & 3]);
-      }
-#pragma unroll
-      for (int i = 0; i < GB; ++i) {
-        float g8[8], x8[8];
-        unpack8v(v[i], g8);
-        unpack8v(v[GB + i], x8);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) g8[e] = fmaf(cA[e], g8[e], fmaf(cB[e], x8[e], cD[e]));
-        u32x4_t o = pack8v(g8);
-        const unsigned msk = ((ok >> i) & 1u) ? 0xffffffffu : 0u;  // padding / rows past M stay zero
-        o.x &= msk;
-        o.y &= msk;
-        o.z &= msk;
-        o.w &= msk;
-        lds_write16(pa[i], o);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      kstep_next<BK>(xr, xs, xci, a.R, a.S, C);
-    }
     if constexpr (PRO) {
       char* sw = smem + (t % NS) * STAGE;
       // one LDS round trip: this stage's scale/shift and the lane's landed pieces together
@@ -781,7 +689,7 @@ __device__ __forceinline__ void conv_fwd_glds_tile(const DrnConvFwdArgs& a, cons
 }
 
 template <int BP, int BC, int WAVES_P, int NS, int NW = 4, bool PF = true, int BK = 64, bool PRO = false,
-          bool SROW = false, bool BNB = false, int NH = 1, bool KS = false, bool IL = false>
+          bool SROW = false, int NH = 1, bool KS = false, bool IL = false>
 __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a, const void* __restrict__ zero) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int lin = xcd_remap(blockIdx.x, gridDim.x);  // (a tile's splits stay on one XCD)
@@ -791,10 +699,10 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_kernel(DrnConvFwdArgs a
     const int t_all = (a.R * a.S * a.C) / BK;
     const int t_beg = (int)((long)ksi * t_all / ksn);
     const int t_cnt = (int)((long)(ksi + 1) * t_all / ksn) - t_beg;
-    conv_fwd_glds_tile<BP, BC, WAVES_P, NS, NW, PF, BK, PRO, SROW, BNB, NH, KS, IL>(a, zero, smem, bid, ksn, ksi, ksn,
-                                                                                  t_beg, t_cnt);
+    conv_fwd_glds_tile<BP, BC, WAVES_P, NS, NW, PF, BK, PRO, SROW, NH, KS, IL>(a, zero, smem, bid, ksn, ksi, ksn, t_beg,
+                                                                             t_cnt);
   } else {
-    conv_fwd_glds_tile<BP, BC, WAVES_P, NS, NW, PF, BK, PRO, SROW, BNB, NH, KS, IL>(a, zero, smem, lin, 1, 0, 1, 0, 0);
+    conv_fwd_glds_tile<BP, BC, WAVES_P, NS, NW, PF, BK, PRO, SROW, NH, KS, IL>(a, zero, smem, lin, 1, 0, 1, 0, 0);
   }
 }
 
@@ -827,7 +735,7 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_sk_kernel(DrnConvFwdArg
     const unsigned bl = __builtin_amdgcn_readfirstlane(owner(tend - 1));
     if (!first) __syncthreads();  // the previous segment's LDS use is over
     // (no epilogue-operand prefetch: most segments end in a partial tile, not an epilogue)
-    conv_fwd_glds_tile<BP, BC, WAVES_P, NS, NW, false, BK, PRO, false, false, NH, true, IL>(
+    conv_fwd_glds_tile<BP, BC, WAVES_P, NS, NW, false, BK, PRO, false, NH, true, IL>(
         a, zero, smem, (int)tile, (int)(bl - bf + 1), (int)(b - bf), a.ksplit, (int)t0, (int)(t1 - t0));
     first = false;
     u = tend;
@@ -1034,7 +942,7 @@ static int nk_cfg_mj(int id) {
 
 static int launch_conv_nk(int id, DrnConvFwdArgs* a, hipStream_t stream) {
   const int mi = nk_cfg_mi(id);
-  if (mi == 0 || a->K != 16 * mi || a->dil != 1 || a->bnb_x != nullptr || a->ksplit > 1 || a->sk_blocks > 0 ||
+  if (mi == 0 || a->K != 16 * mi || a->dil != 1 || a->ksplit > 1 || a->sk_blocks > 0 ||
       a->C < 8 || (a->C & (a->C - 1)) != 0 || (a->R * a->S * a->C + 31) / 32 > 9)
     return (int)hipErrorInvalidValue;
   if (a->in_fin.stats != nullptr && (a->N * a->P * a->Q + 16 * 4 * nk_cfg_mj(id) - 1) / (16 * 4 * nk_cfg_mj(id)) >
@@ -1076,39 +984,25 @@ static int sk_slots(int tiles, int T, int G) {
   return (int)n;
 }
 
-// largest grid that finalizes its input BatchNorm in the prologue (DRN_CFIN_MAX_BLOCKS)
-static int cfin_max_blocks() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DRN_CFIN_MAX_BLOCKS");
-    v = e ? atoi(e) : 2048;
-  }
-  return v;
-}
+// largest grid that finalizes its input BatchNorm in the prologue (profiles/r4_cfin_work_ab.txt)
+static int cfin_max_blocks() { return 2048; }
 
 // ... and a grid whose workgroups would each re-derive many channels: the prologue finalize
 // reads G replicas x C channels per workgroup from L2 (ResNet-50 stage 4: 392 workgroups x 2048
 // channels x 64 B = 51 MB, 8 dependent channel rounds per thread)
-static long cfin_max_work() {
-  static long v = -1;
-  if (v < 0) {
-    const char* e = getenv("DRN_CFIN_MAX_WORK");
-    v = e ? atol(e) : (1L << 19);
-  }
-  return v;
-}
+static long cfin_max_work() { return 1L << 19; }
 
-template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF, int BK, bool PRO, bool SROW = false, bool BNB = false,
-          int NH = 1, bool KS = false, bool IL = false>
+template <int BP, int BC, int WAVES_P, int NS, int NW, bool PF, int BK, bool PRO, bool SROW = false, int NH = 1,
+          bool KS = false, bool IL = false>
 static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
   const int T = a->C == 4 ? (a->R + 1) / 2 : a->C == 8 || a->C == 16 ? a->R : (a->R * a->S * a->C) / BK;  // k-stages
                                                           // (SROW: filter rows; packed stem: row pairs)
-  const int LDS0 = (T < NS ? T : NS) * (BC + BP * (BNB ? 2 : 1)) * BK * 2;  // stage slots actually used
-  const int lds_main = LDS0 + (PRO ? 8 * a->C : 0) + (BNB ? 12 * a->C : 0);  // + fused-BN parameters
+  const int LDS0 = (T < NS ? T : NS) * (BC + BP) * BK * 2;  // stage slots actually used
+  const int lds_main = LDS0 + (PRO ? 8 * a->C : 0);           // + fused-BN parameters
   const int LDS = lds_main > BP * BC * 4 / NH ? lds_main : BP * BC * 4 / NH;  // epilogue staging slice
   if (LDS > 160 * 1024) return (int)hipErrorInvalidValue;
   static bool attr_set = false;
-  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS, NW, PF, BK, PRO, SROW, BNB, NH, KS, IL>;
+  auto kern = conv_fwd_glds_kernel<BP, BC, WAVES_P, NS, NW, PF, BK, PRO, SROW, NH, KS, IL>;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
@@ -1158,15 +1052,15 @@ static int launch_conv_glds_nh1(DrnConvFwdArgs* a, const void* zero, hipStream_t
 // split-K launch (a->ksplit > 1): plain / fused-BN-prologue inputs only
 template <int BP, int BC, int WAVES_P, int NS, int NW, int BK, int NH, bool IL>
 static int launch_conv_glds_ks(DrnConvFwdArgs* a, const void* zero, hipStream_t stream) {
-  if (a->C == 4 || a->C == 8 || a->C == 16 || a->C % BK || a->bnb_x != nullptr) return (int)hipErrorInvalidValue;
+  if (a->C == 4 || a->C == 8 || a->C == 16 || a->C % BK) return (int)hipErrorInvalidValue;
   // epilogue operands: prefetched by the (NH == 1) kernels that keep them in registers
   constexpr bool PFOK = NH == 1;
   const bool pf = PFOK && (a->residual != nullptr || a->bn_x != nullptr);
   if (a->in_scale != nullptr)
-    return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, PFOK, BK, true, false, false, NH, true, IL>(a, zero, stream)
-              : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, true, false, false, NH, true, IL>(a, zero, stream);
-  return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, PFOK, BK, false, false, false, NH, true, IL>(a, zero, stream)
-            : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false, false, false, NH, true, IL>(a, zero, stream);
+    return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, PFOK, BK, true, false, NH, true, IL>(a, zero, stream)
+              : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, true, false, NH, true, IL>(a, zero, stream);
+  return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, PFOK, BK, false, false, NH, true, IL>(a, zero, stream)
+            : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false, false, NH, true, IL>(a, zero, stream);
 }
 
 // epilogue operands (residual / BN-backward input) are prefetched only when present
@@ -1177,10 +1071,10 @@ static int launch_conv_glds(DrnConvFwdArgs* a, const void* zero, hipStream_t str
     return (int)hipErrorInvalidValue;
   }
   if constexpr (NH > 1) {  // big tiles: plain / fused-BN-prologue input, sliced epilogue, no prefetch
-    if (a->C == 4 || a->C == 8 || a->C == 16 || a->C % BK || a->bnb_x != nullptr) return (int)hipErrorInvalidValue;
+    if (a->C == 4 || a->C == 8 || a->C == 16 || a->C % BK) return (int)hipErrorInvalidValue;
     if (a->in_scale != nullptr)
-      return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, true, false, false, NH, false, IL>(a, zero, stream);
-    return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false, false, false, NH, false, IL>(a, zero, stream);
+      return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, true, false, NH, false, IL>(a, zero, stream);
+    return launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false, false, NH, false, IL>(a, zero, stream);
   } else {
     return launch_conv_glds_nh1<BP, BC, WAVES_P, NS, NW, BK, IL>(a, zero, stream);
   }
@@ -1202,17 +1096,11 @@ static int launch_conv_glds_nh1(DrnConvFwdArgs* a, const void* zero, hipStream_t
     return (int)hipErrorInvalidValue;
   }
   if (a->C % BK) return (int)hipErrorInvalidValue;
-  if (a->bnb_x != nullptr) {  // fused BN-backward input (data gradients): 64-deep stages only
-    if constexpr (BK == 64)
-      return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, false, false, true, 1, false, IL>(a, zero, stream)
-                : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false, false, true, 1, false, IL>(a, zero, stream);
-    return (int)hipErrorInvalidValue;
-  }
   if (a->in_scale != nullptr)
-    return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, true, false, false, 1, false, IL>(a, zero, stream)
-              : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, true, false, false, 1, false, IL>(a, zero, stream);
-  return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, false, false, false, 1, false, IL>(a, zero, stream)
-            : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false, false, false, 1, false, IL>(a, zero, stream);
+    return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, true, false, 1, false, IL>(a, zero, stream)
+              : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, true, false, 1, false, IL>(a, zero, stream);
+  return pf ? launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, true, BK, false, false, 1, false, IL>(a, zero, stream)
+            : launch_conv_glds_pf<BP, BC, WAVES_P, NS, NW, false, BK, false, false, 1, false, IL>(a, zero, stream);
 }
 
 // Tile configurations of the LDS-DMA kernel (index = DRN conv config id, also used by the
@@ -1362,8 +1250,6 @@ DRN_API int drn_conv_fwd(DrnConvFwdArgs* a, hipStream_t s);
 
 // Whether the LDS-DMA kernel family supports this convolution.
 DRN_API int drn_conv_glds_ok(const DrnConvFwdArgs* a) {
-  if (a->bnb_x != nullptr)  // fused BN-backward input: LDS-DMA 64-deep stages only
-    return a->C % 64 == 0 && a->C <= 4096 && a->dil == 1 && a->in_scale == nullptr;
   if (a->C == 4)  // packed stem (stem.hip): tap pairs of 4 channels, two filter rows per stage
     return a->dil == 1 && a->S % 2 == 0 && a->S * a->C <= 32 && a->in_scale == nullptr && a->bn_x == nullptr &&
            a->residual == nullptr;
@@ -1389,8 +1275,6 @@ DRN_API int drn_conv_fwd2(DrnConvFwdArgs* a, const void* zero, hipStream_t s) {
     return (int)hipErrorInvalidValue;  // split-K: explicit split-capable LDS-DMA configurations only
   if (a->cfg >= DRN_NK_CFG0 && a->cfg < DRN_NK_CFG0 + DRN_NK_NCFG) return drn::launch_conv_nk(a->cfg - DRN_NK_CFG0, a, s);
   if (a->cfg >= DRN_GLDS_NCFG && a->cfg != 100) return (int)hipErrorInvalidValue;
-  if (a->bnb_x != nullptr && (!drn_conv_glds_ok(a) || zero == nullptr || a->cfg == 100))
-    return (int)hipErrorInvalidValue;  // the BN-backward input transform exists on the LDS-DMA path only
   if (drn_conv_glds_ok(a) && zero != nullptr && a->cfg != 100)
     return drn::launch_glds_cfg(a->cfg >= 0 ? a->cfg : drn::glds_default_cfg(a), a, zero, s);
   if (a->in_fin.stats != nullptr) {
@@ -1414,6 +1298,8 @@ DRN_API int drn_conv_trace_set(unsigned long long* buf) {
 
 DRN_API int drn_conv_glds_cfg_bp(int cfg) { return drn::glds_cfg_bp(cfg); }
 DRN_API int drn_conv_glds_cfg_bc(int cfg) { return drn::glds_cfg_bc(cfg); }
+// k depth of a split-capable configuration's stages (0: not split-K / stream-K capable)
+DRN_API int drn_conv_glds_cfg_bk(int cfg) { return drn::glds_cfg_bk(cfg); }
 // partial slots per tile a stream-K launch of split-capable config cfg with G workgroups needs
 // (0: not split-capable, or more workgroups than tile x k-stage units)
 DRN_API int drn_conv_sk_slots_cfg(const DrnConvFwdArgs* a, int cfg, int G) {

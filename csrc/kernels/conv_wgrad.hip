@@ -24,10 +24,6 @@
 #include "drn_conv.h"
 #include <stdlib.h>
 
-#ifndef DRN_WGRAD_STAGES
-#define DRN_WGRAD_STAGES 2
-#endif
-
 namespace drn {
 
 // Per-workgroup timeline of the LDS-DMA weight-gradient kernel, compiled in only with
@@ -43,12 +39,6 @@ __device__ __forceinline__ unsigned long long wg_realtime() {
 #endif
 
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, const DrnFastDiv& f) { return drn_fdiv(n, f); }
-
-// A/B switch read once per process (e.g. DRN_WGRAD_LIN=0 restores the generic patch loader)
-static bool getenv_flag(const char* name, bool dflt) {
-  const char* e = getenv(name);
-  return e == nullptr ? dflt : atoi(e) != 0;
-}
 
 // 32-byte-slot swizzle for rows of W bytes (W = 64, 128 or 256). W = 64 (the narrow 32-channel
 // dY image of the K <= 32 weight gradients): 2 slots per row; the transposed fragment reads of
@@ -121,7 +111,6 @@ __global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_wgrad_kernel(DrnCo
   const int Ktot = a.R * a.S * a.C;
   const int M = a.N * a.P * a.Q;
   const int nkt = (Ktot + BKK - 1) / BKK;
-#ifndef DRN_WGRAD_NO_XCD_REMAP
   // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs by linear id, so the
   // (k-tile, channel-tile) blocks of one pixel split -- which all read the same pixels of x and
   // dY -- would land on different XCDs and fetch them into 8 different L2s. Remapping the linear
@@ -130,10 +119,6 @@ __global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_wgrad_kernel(DrnCo
   const int lin = xcd_remap(blockIdx.x + blockIdx.y * ntile, ntile * gridDim.y);
   const int tile = lin % ntile;
   const int split = lin / ntile;
-#else
-  const int tile = blockIdx.x;
-  const int split = blockIdx.y;
-#endif
   const int kt = tile % nkt;
   const int ct = tile / nkt;
   const int k0 = kt * BKK, c0 = ct * BCO;
@@ -284,7 +269,7 @@ __global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_wgrad_kernel(DrnCo
 
 template <int BKK, int BCO, bool PRO>
 static int launch_wgrad(DrnConvWgradArgs* a, hipStream_t s) {
-  constexpr int NST = DRN_WGRAD_STAGES;
+  constexpr int NST = 2;
   constexpr int LDS = NST * (64 * BKK * 2 + 64 * BCO * 2);
   static bool attr_set = false;
   auto kern = conv_wgrad_kernel<BKK, BCO, PRO, NST>;
@@ -367,12 +352,6 @@ __device__ __forceinline__ void lgkm_fence(s16x4v (&a)[MI][2], s16x4v (&b)[MJ][2
 // lane's channels are fixed for the whole kernel, so scale/shift stay in registers) and the
 // stage's barrier publishes them. Zero-page pieces (padding, pixels past the split) stay zero.
 //
-// BNB: dY is dx of a BatchNorm whose apply was not materialised (DrnConvWgradArgs::bnb_x):
-// each stage also DMAs the BatchNorm-input pieces (an X image behind the dY image) and every
-// lane rewrites its own landed dY pieces as A*g + B*x + D (its 8 channels are fixed for the
-// kernel, so the coefficients live in registers; they are finalized once per workgroup from the
-// backward statistics); pieces past the split / the channel range stay zero.
-//
 // IL: the next stage's LDS-DMA pieces are issued one at a time between this stage's MFMAs
 // (instead of all right after the barrier, where every wave issues in lockstep and the matrix
 // pipe idles for the DMA issue time).
@@ -387,17 +366,17 @@ __device__ __forceinline__ void lgkm_fence(s16x4v (&a)[MI][2], s16x4v (&b)[MJ][2
 // LIN: 1x1 stride-1 unpadded convolutions (33 of ResNet-50's 53 weight gradients): the patch row
 // of pixel m is x[m][k0..] itself, so the patch loader is as cheap as the dY loader (no pixel
 // decode, no padding test).
-template <int BKK, int BCO, int NS, int BP = 64, bool PRO = false, bool BNB = false, bool IL = false, bool LIN = false>
+template <int BKK, int BCO, int NS, int BP = 64, bool PRO = false, bool IL = false, bool LIN = false>
 __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a, const void* __restrict__ zero) {
   static_assert(BP == 32 || BP == 64, "pixels per stage");
   constexpr int KS = BP / 32;  // 32-deep MFMA k-slices per stage
   constexpr int WA = BKK * 2, WB = BCO * 2;       // image row bytes
   constexpr int A_BYTES = BP * WA;
-  constexpr int STAGE = A_BYTES + BP * WB * (BNB ? 2 : 1);
+  constexpr int STAGE = A_BYTES + BP * WB;
   constexpr int LPA = WA / 16, LPB = WB / 16;     // lanes per row in one wave-instruction
   constexpr int RIA = 64 / LPA, RIB = 64 / LPB;   // rows per wave-instruction
   constexpr int IA = BP / RIA / 4, IB = BP / RIB / 4;  // instructions per wave per stage
-  constexpr int G = IA + IB * (BNB ? 2 : 1);
+  constexpr int G = IA + IB;
   constexpr int D = NS - 1;
   constexpr int WKK = BKK / 2, WCO = BCO / 2;
   constexpr int MI = WKK / 16, MJ = WCO / 16;
@@ -415,7 +394,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
   const int Ktot = a.R * a.S * a.C;
   const int M = a.N * a.P * a.Q;
   const int nkt = (Ktot + BKK - 1) / BKK;
-#ifndef DRN_WGRAD_NO_XCD_REMAP
   // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs by linear id, so the
   // (k-tile, channel-tile) blocks of one pixel split -- which all read the same pixels of x and
   // dY -- would land on different XCDs and fetch them into 8 different L2s. Remapping the linear
@@ -424,10 +402,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
   const int lin = xcd_remap(blockIdx.x + blockIdx.y * ntile, ntile * gridDim.y);
   const int tile = lin % ntile;
   const int split = lin / ntile;
-#else
-  const int tile = blockIdx.x;
-  const int split = blockIdx.y;
-#endif
   const int kt = tile % nkt;
   const int ct = tile / nkt;
   const int k0 = kt * BKK, c0 = ct * BCO;
@@ -479,42 +453,17 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
   const bool cvalid = dc < a.K;
   const bf16_t* __restrict__ xg = reinterpret_cast<const bf16_t*>(a.x);
   const bf16_t* __restrict__ dyg = reinterpret_cast<const bf16_t*>(a.dy) + dc;
-  const bf16_t* __restrict__ bxg = BNB ? reinterpret_cast<const bf16_t*>(a.bnb_x) + dc : nullptr;
   static_assert(!(LIN && IL), "LIN: plain stage issue only");
   // uniform fast-path conditions (every lane's k / output-channel chunk in range) and the per-lane
   // element offsets of the pieces inside a stage (stage base = uniform pixel offset)
   const bool a_full = k0 + BKK <= Ktot, b_full = c0 + BCO <= a.K;
   const bf16_t* __restrict__ dy0 = reinterpret_cast<const bf16_t*>(a.dy);
-  const bf16_t* __restrict__ bx0 = BNB ? reinterpret_cast<const bf16_t*>(a.bnb_x) : nullptr;
   uint32_t offB[IB], offA[LIN ? IA : 1];
 #pragma unroll
   for (int i = 0; i < IB; ++i) offB[i] = (uint32_t)((RIB * (wave + 4 * i) + brow) * a.K + dc);
   if constexpr (LIN) {
 #pragma unroll
     for (int i = 0; i < IA; ++i) offA[i] = (uint32_t)((RIA * (wave + 4 * i) + arow) * a.C + kk);
-  }
-  float bA[8], bB[8], bD[8];  // BNB: this lane's 8 dY channels' coefficients
-  if constexpr (BNB) {
-    // finalize the block's BCO channels into LDS (behind the pipeline stages), then each lane
-    // takes its 8; retired before any LDS-DMA is in flight
-    float* cf = reinterpret_cast<float*>(smem + NS * STAGE);
-    for (int cl = threadIdx.x; cl < BCO; cl += 256) {
-      const int c = c0 + cl;
-      float A = 0.f, B = 0.f, D = 0.f;
-      if (c < a.K) drn_bn_fin_bwd(a.bnb_fin, c, false, A, B, D);
-      cf[cl] = A;
-      cf[BCO + cl] = B;
-      cf[2 * BCO + cl] = D;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      bA[e] = cf[blc * 8 + e];
-      bB[e] = cf[BCO + blc * 8 + e];
-      bD[e] = cf[2 * BCO + blc * 8 + e];
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) asm volatile("" : "+v"(bA[e]), "+v"(bB[e]), "+v"(bD[e]));
   }
   // Pixel coordinates of this lane's A rows, decoded once and then advanced by 64 pixels per
   // stage with adds/compares (a magic-number division per row per stage made the loader
@@ -555,32 +504,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
   // one 64-pixel step (shared by issue() and the interleaved issue_piece())
   auto a_piece = [&](char* st, int slot, int i, bool full) {
     const int r0 = RIA * (wave + 4 * i);
-#ifdef DRN_WGRAD_GENERIC_DECODE  // A/B: the per-step pixel decode of the previous revision
-    {
-      const int h = __mul24(ap[i], a.stride) + roff;
-      const int w = __mul24(aq[i], a.stride) + soff;
-      const bool ok = kvalid && am[i] < mend && (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
-      const uint32_t off = (uint32_t)(__mul24(an[i], HWC) + __mul24(h, WC) + __mul24(w, a.C) + ci);
-      const void* src = ok ? (const void*)(xg + off) : zero;
-      if constexpr (PRO) {
-        const uint32_t bit = 1u << (slot * IA + i);
-        okm = ok ? (okm | bit) : (okm & ~bit);
-      }
-      __builtin_amdgcn_global_load_lds((wg_gbl_void*)src, (wg_lds_void*)(st + r0 * WA), 16, 0, 0);
-      am[i] += BP;
-      aq[i] += dq;
-      ap[i] += dp;
-      if (aq[i] >= a.Q) {
-        aq[i] -= a.Q;
-        ++ap[i];
-      }
-      while (ap[i] >= a.P) {
-        ap[i] -= a.P;
-        ++an[i];
-      }
-      return;
-    }
-#endif
     // (bitwise, not short-circuit: one select per piece instead of exec-mask branches)
     const bool ok = kvalid & (full | (am[i] < mend)) & ((unsigned)hh[i] < (unsigned)a.H) &
                     ((unsigned)ww[i] < (unsigned)a.W);
@@ -607,11 +530,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
 
   auto issue = [&](int slot, int mstep) {
     char* st = smem + slot * STAGE;
-#ifndef DRN_NO_FAST_LOADER
     const bool full = mstep + BP <= mend;  // wave-uniform: no piece of this stage is past the split
-#else
-    const bool full = false;
-#endif
     if constexpr (LIN) {
       const bf16_t* __restrict__ xs = xg + (size_t)mstep * a.C;
       if (full && a_full) {
@@ -636,18 +555,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
 #pragma unroll
     for (int i = 0; i < (LIN ? 0 : IA); ++i) a_piece(st, slot, i, full);
     const bf16_t* __restrict__ ds = dy0 + (size_t)mstep * a.K;
-    const bf16_t* __restrict__ xbs = BNB ? bx0 + (size_t)mstep * a.K : nullptr;
     if (full && b_full) {
 #pragma unroll
       for (int i = 0; i < IB; ++i)
         __builtin_amdgcn_global_load_lds((wg_gbl_void*)(ds + offB[i]), (wg_lds_void*)(st + A_BYTES + RIB * (wave + 4 * i) * WB),
                                          16, 0, 0);
-      if constexpr (BNB) {
-#pragma unroll
-        for (int i = 0; i < IB; ++i)
-          __builtin_amdgcn_global_load_lds((wg_gbl_void*)(xbs + offB[i]),
-                                           (wg_lds_void*)(st + A_BYTES + BP * WB + RIB * (wave + 4 * i) * WB), 16, 0, 0);
-      }
     } else {
 #pragma unroll
       for (int i = 0; i < IB; ++i) {
@@ -656,37 +568,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
         __builtin_amdgcn_global_load_lds((wg_gbl_void*)(ok ? (const void*)(ds + offB[i]) : zero),
                                          (wg_lds_void*)(st + A_BYTES + r0 * WB), 16, 0, 0);
       }
-      if constexpr (BNB) {
-#pragma unroll
-        for (int i = 0; i < IB; ++i) {
-          const int r0 = RIB * (wave + 4 * i);
-          const bool ok = cvalid && mstep + r0 + brow < mend;
-          __builtin_amdgcn_global_load_lds((wg_gbl_void*)(ok ? (const void*)(xbs + offB[i]) : zero),
-                                           (wg_lds_void*)(st + A_BYTES + BP * WB + r0 * WB), 16, 0, 0);
-        }
-      }
     }
   };
 
-  // one piece of issue(): g < IA: patch piece g (and its pixel-state advance); then the dY
-  // pieces, then the BatchNorm-input pieces
+  // one piece of issue(): g < IA: patch piece g (and its pixel-state advance); then the dY pieces
   auto issue_piece = [&](int slot, int mstep, int gp) {
     char* st = smem + slot * STAGE;
     if (gp < IA) {
       a_piece(st, slot, gp, false);
       return;
     }
-    const int i = (gp - IA) % IB;
+    const int i = gp - IA;
     const int r0 = RIB * (wave + 4 * i);
     const int m = mstep + r0 + brow;
     const bool ok = cvalid && m < mend;
-    if (gp < IA + IB) {
-      __builtin_amdgcn_global_load_lds((wg_gbl_void*)(ok ? (const void*)(dyg + (uint32_t)__mul24(m, a.K)) : zero),
-                                       (wg_lds_void*)(st + A_BYTES + r0 * WB), 16, 0, 0);
-    } else if constexpr (BNB) {
-      __builtin_amdgcn_global_load_lds((wg_gbl_void*)(ok ? (const void*)(bxg + (uint32_t)__mul24(m, a.K)) : zero),
-                                       (wg_lds_void*)(st + A_BYTES + BP * WB + r0 * WB), 16, 0, 0);
-    }
+    __builtin_amdgcn_global_load_lds((wg_gbl_void*)(ok ? (const void*)(dyg + (uint32_t)__mul24(m, a.K)) : zero),
+                                     (wg_lds_void*)(st + A_BYTES + r0 * WB), 16, 0, 0);
   };
 
 
@@ -728,37 +625,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
       }
       lds_wait_all<IA>(v);
       lds_bn_relu_store<IA, true>(pa, v, (okm >> (slot * IA)) & ((1u << IA) - 1u), psc2, psh2);
-    }
-    if constexpr (BNB) {
-      const int slot = t % NS;
-      char* sw = smem + slot * STAGE + A_BYTES;
-      const int mstep = mbeg + t * BP;
-      uint32_t pb[IB];
-      u32x4_t v[2 * IB];
-#pragma unroll
-      for (int i = 0; i < IB; ++i) {
-        pb[i] = lds_addr(sw + RIB * (wave + 4 * i) * WB + lane * 16);
-        v[i] = lds_read16(pb[i]);
-        v[IB + i] = lds_read16(pb[i] + BP * WB);
-      }
-      lds_wait_all<2 * IB>(v);
-#pragma unroll
-      for (int i = 0; i < IB; ++i) {
-        float g8[8], x8[8];
-        unpack8v(v[i], g8);
-        unpack8v(v[IB + i], x8);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) g8[e] = fmaf(bA[e], g8[e], fmaf(bB[e], x8[e], bD[e]));
-        u32x4_t o = pack8v(g8);
-        const bool ok = cvalid && mstep + RIB * (wave + 4 * i) + brow < mend;
-        const unsigned msk = ok ? 0xffffffffu : 0u;
-        o.x &= msk;
-        o.y &= msk;
-        o.z &= msk;
-        o.w &= msk;
-        lds_write16(pb[i], o);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -845,11 +711,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
 #endif
 }
 
-template <int BKK, int BCO, int NS, int BP, bool PRO, bool BNB = false, bool IL = false, bool LIN = false>
+template <int BKK, int BCO, int NS, int BP, bool PRO, bool IL = false, bool LIN = false>
 static int launch_wgrad_glds_p(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
-  constexpr int LDS = NS * (BP * BKK * 2 + BP * BCO * 2 * (BNB ? 2 : 1)) + (BNB ? 12 * BCO : 0);
+  constexpr int LDS = NS * (BP * BKK * 2 + BP * BCO * 2);
   static bool attr_set = false;
-  auto kern = conv_wgrad_glds_kernel<BKK, BCO, NS, BP, PRO, BNB, IL, LIN>;
+  auto kern = conv_wgrad_glds_kernel<BKK, BCO, NS, BP, PRO, IL, LIN>;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr_set = true;
@@ -876,29 +742,16 @@ static int launch_wgrad_glds(DrnConvWgradArgs* a, const void* zero, hipStream_t 
 
 template <int BKK, int BCO, int NS, int BP, bool IL>
 static int launch_wgrad_glds_ok(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
-#ifndef DRN_NO_FAST_LOADER
-  static const bool lin_on = getenv_flag("DRN_WGRAD_LIN", true);
-#else
-  static const bool lin_on = false;
-#endif
-  const bool lin = !IL && lin_on && a->R == 1 && a->S == 1 && a->stride == 1 && a->pad_h == 0 && a->pad_w == 0 &&
+  const bool lin = !IL && a->R == 1 && a->S == 1 && a->stride == 1 && a->pad_h == 0 && a->pad_w == 0 &&
                    a->C % 8 == 0;
   if constexpr (!IL) {
     if (lin) {
-      if (a->bnb_x != nullptr) {
-        if (a->in_scale != nullptr) return launch_wgrad_glds_p<BKK, BCO, NS, BP, true, true, false, true>(a, zero, s);
-        return launch_wgrad_glds_p<BKK, BCO, NS, BP, false, true, false, true>(a, zero, s);
-      }
-      if (a->in_scale != nullptr) return launch_wgrad_glds_p<BKK, BCO, NS, BP, true, false, false, true>(a, zero, s);
-      return launch_wgrad_glds_p<BKK, BCO, NS, BP, false, false, false, true>(a, zero, s);
+      if (a->in_scale != nullptr) return launch_wgrad_glds_p<BKK, BCO, NS, BP, true, false, true>(a, zero, s);
+      return launch_wgrad_glds_p<BKK, BCO, NS, BP, false, false, true>(a, zero, s);
     }
   }
-  if (a->bnb_x != nullptr) {
-    if (a->in_scale != nullptr) return launch_wgrad_glds_p<BKK, BCO, NS, BP, true, true, IL>(a, zero, s);
-    return launch_wgrad_glds_p<BKK, BCO, NS, BP, false, true, IL>(a, zero, s);
-  }
-  if (a->in_scale != nullptr) return launch_wgrad_glds_p<BKK, BCO, NS, BP, true, false, IL>(a, zero, s);
-  return launch_wgrad_glds_p<BKK, BCO, NS, BP, false, false, IL>(a, zero, s);
+  if (a->in_scale != nullptr) return launch_wgrad_glds_p<BKK, BCO, NS, BP, true, IL>(a, zero, s);
+  return launch_wgrad_glds_p<BKK, BCO, NS, BP, false, IL>(a, zero, s);
 }
 
 template <int NS, int BP, bool IL = false>
@@ -1016,7 +869,6 @@ DRN_API int drn_wgrad_tiles(int Ktot, int K) {
 DRN_API int drn_conv_wgrad(DrnConvWgradArgs* a, hipStream_t s) {
   if ((a->C % 8) != 0 || (a->K % 8) != 0 || a->splits < 1 || (a->pix_per_split % 64) != 0)
     return (int)hipErrorInvalidValue;
-  if (a->bnb_x != nullptr) return (int)hipErrorInvalidValue;  // BN-backward dY: LDS-DMA kernels only
   return a->in_scale != nullptr ? drn::dispatch_wgrad<true>(a, s) : drn::dispatch_wgrad<false>(a, s);
 }
 
@@ -1024,13 +876,10 @@ DRN_API int drn_conv_wgrad(DrnConvWgradArgs* a, hipStream_t s) {
 DRN_API int drn_conv_wgrad2(DrnConvWgradArgs* a, const void* zero, int ns, hipStream_t s) {
   // C == 4: the packed stem (stem.hip) -- every 16-byte k piece is a tap pair x 4 channels, so the
   // tap count must be even (S padded to 8); LDS-DMA kernels, no fused prologue
-  const bool packed = a->C == 4 && a->S % 2 == 0 && a->in_scale == nullptr && a->bnb_x == nullptr && zero != nullptr &&
-                      ns != 0;
+  const bool packed = a->C == 4 && a->S % 2 == 0 && a->in_scale == nullptr && zero != nullptr && ns != 0;
   if (((a->C % 8) != 0 && !packed) || (a->K % 8) != 0 || a->splits < 1 || (a->pix_per_split % 64) != 0)
     return (int)hipErrorInvalidValue;
-  // the LDS-DMA kernels' fused BN prologue always applies the ReLU (pre-activation v2)
-  if (a->bnb_x != nullptr && (zero == nullptr || ns == 0 || (a->in_scale != nullptr && a->relu_in == 0)))
-    return (int)hipErrorInvalidValue;
+  // (the LDS-DMA kernels' fused BN prologue always applies the ReLU: pre-activation v2)
   if (zero == nullptr || ns == 0 || (a->in_scale != nullptr && a->relu_in == 0)) return drn_conv_wgrad(a, s);
   return drn::dispatch_wgrad_glds(a, zero, ns, s);
 }

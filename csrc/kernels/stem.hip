@@ -4,7 +4,7 @@
 // every loader), so the stem's reduction k = (r, s, c) over 7 x 7 x 8 is 62.5 % zero channels:
 // the forward ran 7 LDS-DMA stages of 64 (one filter row each) and the weight gradient 4 k-tiles
 // of 128 for 147 useful k (reference resnet_model_official.py:301-306, the 7x7/2 stem conv).
-// Packed stem (executor DRN_STEM_PACK): the input is re-laid out once per step as
+// Packed stem (Executor.stem_pack): the input is re-laid out once per step as
 //   xp[n][h][1 + w][c4]   (4 channels, one zero pixel column on each side of every row),
 // so one 16-byte piece = TWO horizontally adjacent taps x 4 channels; with the filter padded to
 // S = 8 taps (tap 7 zero) a filter row is 4 pieces and a 64-deep stage holds TWO filter rows:

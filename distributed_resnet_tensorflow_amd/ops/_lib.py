@@ -63,7 +63,6 @@ class DrnConvFwdArgs(ctypes.Structure):
         ("fin_scale", c_p), ("fin_shift", c_p), ("fin_mean", c_p), ("fin_invstd", c_p),
         ("fin_dgamma", c_p), ("fin_dbeta", c_p), ("fin_coef", c_p),
         ("fd_pq", DrnFastDiv), ("fd_q", DrnFastDiv), ("in_fin", DrnBnFin),
-        ("bnb_x", c_p), ("bnb_fin", DrnBnFin),
         ("ks_ws", c_p), ("ks_tickets", c_p), ("ksplit", c_int), ("sk_blocks", c_int),
     ]
 
@@ -74,7 +73,7 @@ class DrnConvWgradArgs(ctypes.Structure):
         ("N", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("K", c_int), ("R", c_int), ("S", c_int),
         ("P", c_int), ("Q", c_int), ("stride", c_int), ("pad_h", c_int), ("pad_w", c_int), ("relu_in", c_int),
         ("splits", c_int), ("pix_per_split", c_int), ("fd_pq", DrnFastDiv), ("fd_q", DrnFastDiv),
-        ("bnb_x", c_p), ("bnb_fin", DrnBnFin), ("atomic_out", c_int),
+        ("atomic_out", c_int),
     ]
 
 
@@ -126,6 +125,8 @@ _SIGS = {
     "drn_p2p_cast": ([c_p, c_p, c_i64, c_p], c_int),
     "drn_p2p_args_size": ([], c_int),
     "drn_conv_glds_cfg_bc": ([c_int], c_int),
+    "drn_conv_glds_cfg_bp": ([c_int], c_int),
+    "drn_conv_glds_cfg_bk": ([c_int], c_int),
     "drn_conv_sk_slots_cfg": ([c_p, c_int, c_int], c_int),
     "drn_conv_nk_num_cfgs": ([], c_int),
     "drn_conv_nk_cfg0": ([], c_int),

@@ -218,7 +218,7 @@ class HipBackend(_Common):
     acc_dtype = torch.float32
     # replicas of every BN statistics accumulator: producer block b adds into replica b % R,
     # the finalize kernels sum them (same-address fp32 atomics serialize at ~15 ns each)
-    stats_replicas = int(os.environ.get("DRN_STATS_REPLICAS", "8"))  # measured: 8 ~ 4 < 16 < 32 < 64
+    stats_replicas = 8  # measured: 8 ~ 4 < 16 < 32 < 64
 
     def __init__(self, device="cuda"):
         self.device = torch.device(device)
@@ -231,11 +231,11 @@ class HipBackend(_Common):
         # any graph capture: the autotuner sizes it) and one ticket word per output tile
         self.ks_ws = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.ks_tickets = torch.zeros(1 << 16, dtype=torch.int32, device=self.device)
-        self.KS_FACTORS = tuple(int(v) for v in os.environ.get("DRN_CONV_KSPLIT", "2,3,4").split(",") if v)
+        self.KS_FACTORS = (2, 3, 4)
         # stream-K grid sizes tried by the autotuner (256 CUs: 1 or 2 resident workgroups each)
-        self.SK_BLOCKS = tuple(int(v) for v in os.environ.get("DRN_CONV_SK", "256,512").split(",") if v)
-        forced = os.environ.get("DRN_CONV_CFG")
-        self.forced_cfg = int(forced) if forced not in (None, "") else None
+        self.SK_BLOCKS = (256, 512)
+        # a fixed configuration for every conv (tests / experiments set it; None = autotune)
+        self.forced_cfg = None
         self.autotune = os.environ.get("DRN_AUTOTUNE", "1") == "1"
         self.wgrad_ns: dict = {}
         # split-K by fp32 atomics into the gradient is a tuner candidate only once the executor
@@ -243,8 +243,7 @@ class HipBackend(_Common):
         # wgrad_atomic_used when some layer picked it
         self.wgrad_atomic_ok = False
         self.wgrad_atomic_used = False
-        forced = os.environ.get("DRN_WGRAD_NS")
-        self.forced_wgrad_ns = int(forced) if forced not in (None, "") else None
+        self.forced_wgrad_ns = None  # a fixed weight-gradient pipeline (tests / experiments)
         self.tune_log: list = []
         self._db = None   # persistent kernel-selection database (ops/tunedb.py), loaded on first use
         self.db_hits = 0
@@ -282,7 +281,7 @@ class HipBackend(_Common):
 
     # -- conv ---------------------------------------------------------------------------------
     def conv_args(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None,
-                  bn_bwd=None, bn_fin: Optional[BnFin] = None, in_fin: Optional[BnCfin] = None, bnb=None):
+                  bn_bwd=None, bn_fin: Optional[BnFin] = None, in_fin: Optional[BnCfin] = None):
         N, H, W, C = x.shape
         K, R, S, C2 = w.shape
         N2, P, Q, K2 = y.shape
@@ -331,11 +330,6 @@ class HipBackend(_Common):
             assert in_bn is not None and in_fin.C == C, "the consumer-side finalize feeds the fused BN prologue"
             _aligned16(in_fin.stats)
             a.in_fin = in_fin.struct()
-        if bnb is not None:  # (bn_input, BnCfin): x is the masked BN-backward gradient g
-            bx, bf = bnb
-            assert bx.shape == x.shape and in_bn is None and bf.C == C
-            a.bnb_x = bx.data_ptr()
-            a.bnb_fin = bf.struct()
         cfg, ks = (self.forced_cfg, 1) if self.forced_cfg is not None else self.conv_cfg.get(self.conv_key(a), (-1, 1))
         a.cfg = cfg
         self._set_ksplit(a, ks)
@@ -370,16 +364,40 @@ class HipBackend(_Common):
 
     @staticmethod
     def conv_key(a) -> tuple:
+        """Geometry + every launch property a configuration's validity depends on (fused prologue
+        with / without ReLU, consumer-side finalize replicas, strided output, epilogue operands)."""
         return (a.N, a.H, a.W, a.C, a.K, a.R, a.S, a.P, a.Q, a.stride, a.pad_h, a.pad_w, a.dil,
                 a.in_scale is not None, a.out_stride, a.residual is not None, a.bn_x is not None,
-                a.stats is not None, a.bnb_x is not None)
+                a.stats is not None, int(a.relu_in) if a.in_scale is not None else 0,
+                int(a.in_fin.G) if a.in_fin.stats is not None else 0)
+
+    def _conv_hit_ok(self, a, hit) -> bool:
+        """A database choice is used only if this library can launch it for this geometry now
+        (a known configuration, split-K / stream-K only on split-capable ones; the experiment
+        candidate filter DRN_CONV_CANDS applies to hits too) -- otherwise the geometry is re-tuned."""
+        cfg, ks = hit
+        cands = os.environ.get("DRN_CONV_CANDS")
+        if cands and cfg not in [int(c) for c in cands.split(",")]:
+            return False
+        nk0 = self.L.drn_conv_nk_cfg0()
+        if cfg == 100:
+            return ks == 1
+        if nk0 <= cfg < nk0 + self.L.drn_conv_nk_num_cfgs():
+            return ks == 1 and a.K in (16, 32)
+        if not (0 <= cfg < self.L.drn_conv_glds_num_cfgs()) or not self.L.drn_conv_glds_ok(ctypes.byref(a)):
+            return False
+        if ks > 1:
+            return self.L.drn_conv_glds_cfg_bk(cfg) > 0 and a.out_stride == 0
+        if ks < 0:
+            return a.out_stride == 0 and self.L.drn_conv_sk_slots_cfg(ctypes.byref(a), cfg, -ks) > 0
+        return True
 
     def launch_conv(self, a):
         if a.cfg == -1 and self.autotune and self.forced_cfg is None:
             key = self.conv_key(a)
             if key not in self.conv_cfg and not torch.cuda.is_current_stream_capturing():
                 hit = self.tune_db().get_conv(key)
-                if hit is not None:
+                if hit is not None and self._conv_hit_ok(a, hit):
                     self.db_hits += 1
                     self.conv_cfg[key] = hit
                 else:
@@ -424,7 +442,6 @@ class HipBackend(_Common):
             t.stats = st.data_ptr()
         t.fin_cnt = None  # timing runs must not finalize (moving averages) the live BN
         t.in_fin.publish = 0
-        t.bnb_fin.publish = 0
         s = self.stream()
         cands = os.environ.get("DRN_CONV_CANDS")
         if cands:
@@ -468,7 +485,7 @@ class HipBackend(_Common):
                 continue  # configuration not applicable to this geometry (e.g. C % 64 != 0)
             first.append((time_cfg(c, iters), c))
         first.sort()
-        top = {c: ms for ms, c in first[:self.tune_top if os.environ.get("DRN_TUNE_2PASS", "1") == "1" else 1]}
+        top = {c: ms for ms, c in first[:self.tune_top]}
         for _ in range(self.tune_rounds if len(top) > 1 else 0):
             for c in list(top):
                 top[c] = min(top[c], time_cfg(c, 2 * iters))
@@ -479,21 +496,20 @@ class HipBackend(_Common):
         return best
 
     def conv_fwd(self, x, w, y, g, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None, bn_bwd=None,
-                 bn_fin: Optional[BnFin] = None, out_fill: bool = False, in_fin: Optional[BnCfin] = None,
-                 bnb=None):
+                 bn_fin: Optional[BnFin] = None, out_fill: bool = False, in_fin: Optional[BnCfin] = None):
         """y = conv(x) (+ residual); optional BN statistics of y, or (bn_bwd = (x_bn, scale, shift,
         mean, invstd)) the fused BN-backward reduction with ReLU-masked output; bn_fin finalizes
         that BN in the same launch. out_fill (strided out_map, single-phase output): the epilogue
         also writes zeros at every other phase position, so y needs no separate clearing.
         in_fin: the input BN (in_bn) is finalized by this conv's prologue (BnCfin)."""
-        a = self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd, bn_fin, in_fin, bnb)
+        a = self.conv_args(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd, bn_fin, in_fin)
         if out_fill:
             assert out_map is not None and bn_bwd is None and residual is None, "out_fill: plain strided output only"
             a.out_fill = 1
         self.launch_conv(a)
 
-    WGRAD_TARGET_BLOCKS = int(os.environ.get("DRN_WGRAD_TARGET_BLOCKS", "512"))  # measured: 512 > 384, 640, 1024
-    WGRAD_MIN_STEPS = int(os.environ.get("DRN_WGRAD_MIN_STEPS", "8"))
+    WGRAD_TARGET_BLOCKS = 512  # measured: 512 > 384, 640, 1024
+    WGRAD_MIN_STEPS = 8
 
     @staticmethod
     def wgrad_splits(M, Ktot, K, target_blocks: int = 0, min_steps: int = 0):
@@ -518,13 +534,13 @@ class HipBackend(_Common):
     # split-K block targets the wgrad autotuner chooses from per geometry: more splits fill the
     # chip, fewer write (and re-read in drn_splitk_reduce) fewer fp32 partial slabs -- the slab
     # traffic of the default 512-block target is ~1.7 GB per ResNet-50 step
-    WGRAD_TARGETS = tuple(int(v) for v in os.environ.get("DRN_WGRAD_TARGETS", "128,256,384,512,768").split(","))
+    WGRAD_TARGETS = (128, 256, 384, 512, 768)
     # minimum 64-pixel steps per split the tuner also tries: small layers (CIFAR stage 3 at batch
     # 32: 32 steps) otherwise get 4 splits, i.e. 20-64 workgroups walking 8 serial steps each
-    WGRAD_MIN_STEPS_CANDS = tuple(int(v) for v in os.environ.get("DRN_WGRAD_MINSTEPS", "8,2").split(","))
+    WGRAD_MIN_STEPS_CANDS = (8, 2)
 
     def wgrad_args(self, x, dy, out, g: ConvGeom, in_bn=None, relu_in=True, ws=None, target_blocks: int = 0,
-                   bnb=None, atomic: bool = False, min_steps: int = 0):
+                   atomic: bool = False, min_steps: int = 0):
         N, H, W, C = x.shape
         N2, P, Q, K = dy.shape
         Kd, R, S, Cd = out.shape
@@ -541,13 +557,6 @@ class HipBackend(_Common):
         a.splits, a.pix_per_split = splits, pps
         a.fd_pq = _lib.DrnFastDiv.make(P * Q)
         a.fd_q = _lib.DrnFastDiv.make(Q)
-        if bnb is not None:  # dY is the masked BN-backward gradient g; dY_eff = A*g + B*bn_input + D
-            bx, bf = bnb
-            assert bx.shape == dy.shape and bf.C == K
-            a.bnb_x = bx.data_ptr()
-            f = bf.struct()
-            f.publish = 0  # the data-gradient consumer publishes dgamma / dbeta
-            a.bnb_fin = f
         if splits == 1 or atomic:
             a.out = out.data_ptr()
             a.atomic_out = 1 if (atomic and splits > 1) else 0
@@ -569,8 +578,7 @@ class HipBackend(_Common):
 
     @staticmethod
     def wgrad_key(a) -> tuple:
-        return (a.N, a.H, a.W, a.C, a.K, a.R, a.S, a.P, a.Q, a.stride, a.pad_h, a.pad_w, a.in_scale is not None,
-                a.bnb_x is not None)
+        return (a.N, a.H, a.W, a.C, a.K, a.R, a.S, a.P, a.Q, a.stride, a.pad_h, a.pad_w, a.in_scale is not None)
 
     def _wgrad_kernel(self, a, ns: int, st):
         _lib.check(self.L.drn_conv_wgrad2(ctypes.byref(a), self.zero_page.data_ptr(), ns, st), "drn_conv_wgrad")
@@ -604,7 +612,7 @@ class HipBackend(_Common):
             seen.add((a.splits, a.atomic_out))
             for ns in cands:
                 if self.L.drn_conv_wgrad2(ctypes.byref(a), self.zero_page.data_ptr(), ns, st) != 0:
-                    continue  # pipeline not available for this launch (e.g. BN-backward dY: LDS-DMA only)
+                    continue  # pipeline not available for this launch
                 for _ in range(2):
                     self._wgrad_full(a, ns, out, st)
                 first.append((time_one(a, ns, iters), (tgt, ns, bool(a.atomic_out), ms_min), a))
@@ -624,9 +632,8 @@ class HipBackend(_Common):
         self.tune_log.append((("wgrad",) + key, best, round(best_t * 1e3, 1)))
         return best
 
-    def conv_wgrad(self, x, dy, out, g, in_bn=None, relu_in=True, ws=None, bnb=None):
-        args_for = lambda tgt, atomic=False, ms=0: self.wgrad_args(x, dy, out, g, in_bn, relu_in, ws, tgt, bnb, atomic,
-                                                                   ms)
+    def conv_wgrad(self, x, dy, out, g, in_bn=None, relu_in=True, ws=None):
+        args_for = lambda tgt, atomic=False, ms=0: self.wgrad_args(x, dy, out, g, in_bn, relu_in, ws, tgt, atomic, ms)
         a = args_for(0)
         st = self.stream()
         if self.forced_wgrad_ns is not None:
@@ -635,7 +642,8 @@ class HipBackend(_Common):
         key = self.wgrad_key(a)
         if key not in self.wgrad_ns and self.autotune and not torch.cuda.is_current_stream_capturing():
             hit = self.tune_db().get_wgrad(key)
-            if hit is not None and (not hit[2] or self.wgrad_atomic_ok):
+            cands = [int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6,7,8").split(",")]
+            if hit is not None and (not hit[2] or self.wgrad_atomic_ok) and hit[1] in cands:
                 self.db_hits += 1
                 self.wgrad_ns[key] = hit
                 if hit[2]:
@@ -646,8 +654,6 @@ class HipBackend(_Common):
             if self.wgrad_ns[key][2]:
                 self.zero_(out)  # the timing launches left partial sums in this gradient slot
         tgt, ns, atomic, ms = self.wgrad_ns.get(key, (0, 2, False, 0))
-        if ns == 0 and a.bnb_x is not None:
-            ns = 2
         if tgt or atomic or ms:
             a = args_for(tgt, atomic, ms)
         self._wgrad_full(a, ns, out, st)
@@ -656,7 +662,7 @@ class HipBackend(_Common):
     @staticmethod
     def bn_rows_per_block(M, C):
         rpp = max(1, 256 // (C // 8))
-        G_target = int(os.environ.get("DRN_BN_BLOCKS", "512"))
+        G_target = 512
         rpb = max(rpp, ((M + G_target - 1) // G_target + rpp - 1) // rpp * rpp)
         return rpb
 
@@ -728,7 +734,7 @@ class HipBackend(_Common):
     # reads in its prologue (2048 workgroups x 2048 channels x 64 B = 268 MB at the last stage of
     # ResNet-50): from this many channels on, one small finalize launch computes the
     # coefficients once and the apply reads only its own 8 channels'
-    BN_FIN_SPLIT_C = int(os.environ.get("DRN_BN_FIN_SPLIT_C", "1024"))
+    BN_FIN_SPLIT_C = 1024
 
     def _fin_scratch(self, C: int) -> torch.Tensor:
         """[coef 3C][dgamma C][dbeta C] fp32 scratch of the split backward finalize (one per C:
@@ -785,7 +791,7 @@ class HipBackend(_Common):
                                           1 if relu else 0, self.stream()), "drn_bnrelu_pool")
 
     _sgemm_ws: dict = {}
-    SGEMM_TARGET_WG = int(os.environ.get("DRN_SGEMM_TARGET_WG", "256"))
+    SGEMM_TARGET_WG = 256
 
     def sgemm(self, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias=None):
         tiles = ((M + 63) // 64) * ((N + 63) // 64)
@@ -944,12 +950,9 @@ class RefBackend(_Common):
         return None
 
     def conv_fwd(self, x, w, y, g: ConvGeom, in_bn=None, relu_in=True, residual=None, stats=None, out_map=None,
-                 bn_bwd=None, bn_fin: Optional[BnFin] = None, out_fill: bool = False, in_fin: Optional[BnCfin] = None,
-                 bnb=None):
+                 bn_bwd=None, bn_fin: Optional[BnFin] = None, out_fill: bool = False, in_fin: Optional[BnCfin] = None):
         if in_fin is not None and in_fin.publish:
             self._publish_fwd(in_fin)
-        if bnb is not None:
-            x = self._bnb(x, bnb)
         self._conv_fwd(x, w, y, g, in_bn, relu_in, residual, stats, out_map, bn_bwd, out_fill)
         if bn_fin is not None:
             f, G = bn_fin, stats.numel() // (2 * w.shape[0])
@@ -997,25 +1000,7 @@ class RefBackend(_Common):
     def wgrad_ws_elems(self, M, K, R, S, C):
         return 0
 
-    def _bnb(self, gr, bnb, publish: bool = True):
-        """dY of a non-materialised BatchNorm backward (the HIP kernels' BNB prologue):
-        dx = gamma*invstd * (g - mean(g) - xhat * mean(g*xhat)) from the backward statistics
-        replicas, which stay intact for the other consumer; the publishing consumer writes
-        dgamma / dbeta."""
-        bx, f = bnb
-        C = f.C
-        p = f.stats.view(f.G, 2, C).double().sum(0)
-        k1 = (f.gamma * f.invstd).double()
-        xh = (bx.double() - f.mean.double()) * f.invstd.double()
-        dx = k1 * (gr.double() - p[0] / f.count - xh * (p[1] / f.count))
-        if publish and f.publish:
-            f.dbeta.copy_(p[0].to(f.dbeta.dtype))
-            f.dgamma.copy_(p[1].to(f.dgamma.dtype))
-        return dx.to(gr.dtype)
-
-    def conv_wgrad(self, x, dy, out, g: ConvGeom, in_bn=None, relu_in=True, ws=None, bnb=None):
-        if bnb is not None:
-            dy = self._bnb(dy, bnb, publish=False)
+    def conv_wgrad(self, x, dy, out, g: ConvGeom, in_bn=None, relu_in=True, ws=None):
         K, R, S, C = out.shape
         _, P, Q, _ = dy.shape
         xc = _pad_for(_pre(x, in_bn, relu_in).permute(0, 3, 1, 2), P, Q, R, S, g)

@@ -14,11 +14,15 @@ Entries are keyed by
     reuses stale choices, while edits of unrelated kernels (pooling, SGD, BN applies) keep them,
   * the geometry key the backend already uses (conv_key / wgrad_key).
 
-File: ``DRN_TUNE_DB`` (``off`` disables it), default ``ops/tune_db.json`` next to the library, so
-a database produced on an MI355X ships with the tree. Writes are read-merge-write through a
-temporary file and ``os.replace`` (several ranks of one node may write concurrently; the last
-rename wins, every version is a complete file). Sections of other library hashes are dropped
-when a section is written (they can never match again).
+Two files, as MIOpen keeps a system and a user database:
+  * the SYSTEM database ``ops/tune_db.json`` ships with the tree (built on an MI355X by
+    scripts/make_tune_db.py) and is only ever READ: no run, test or bench rewrites it;
+  * the USER database ``DRN_TUNE_DB`` (default ``~/.cache/drn/tune_db.json``) receives every
+    choice this process timed itself; it is consulted for geometries the system database lacks.
+``DRN_TUNE_DB=off`` disables both. Writes are read-merge-write through a temporary file and
+``os.replace`` (several ranks of one node may write concurrently; the last rename wins, every
+version is a complete file). Sections of other library hashes are dropped when a section is
+written (they can never match again).
 """
 from __future__ import annotations
 
@@ -29,15 +33,31 @@ from pathlib import Path
 from typing import Optional
 
 VERSION = 1
-DEFAULT_PATH = Path(__file__).resolve().parent / "tune_db.json"
+SYSTEM_PATH = Path(__file__).resolve().parent / "tune_db.json"
 _LOCK = threading.Lock()
 
 
+def enabled() -> bool:
+    return os.environ.get("DRN_TUNE_DB", "").lower() not in ("off", "0", "none")
+
+
 def db_path() -> Optional[Path]:
-    p = os.environ.get("DRN_TUNE_DB", "")
-    if p.lower() in ("off", "0", "none"):
+    """The writable user database (None when disabled)."""
+    if not enabled():
         return None
-    return Path(p) if p else DEFAULT_PATH
+    p = os.environ.get("DRN_TUNE_DB", "")
+    return Path(p) if p else Path(os.path.expanduser("~")) / ".cache" / "drn" / "tune_db.json"
+
+
+def _load_section(path: Optional[Path], section: str) -> tuple:
+    if path is None or not path.exists():
+        return {}, {}
+    try:
+        data = json.loads(path.read_text())
+        sec = data.get("sections", {}).get(section, {}) if data.get("version") == VERSION else {}
+        return dict(sec.get("conv", {})), dict(sec.get("wgrad", {}))
+    except (OSError, ValueError):
+        return {}, {}
 
 
 def _key(t) -> str:
@@ -45,26 +65,22 @@ def _key(t) -> str:
 
 
 class TuneDB:
-    """One section (device + library) of the database, loaded lazily."""
+    """One section (device + library) of the databases: lookups read the system database first,
+    then the user database; new choices go to the user database only."""
 
-    def __init__(self, section: str, path: Optional[Path] = None):
+    def __init__(self, section: str, path: Optional[Path] = None, system: Optional[Path] = None):
         self.section = section
         self.path = db_path() if path is None else path
-        self.conv: dict = {}
-        self.wgrad: dict = {}
+        on = enabled() or path is not None
+        self.sys_conv, self.sys_wgrad = _load_section(SYSTEM_PATH if system is None else system, section) if on \
+            else ({}, {})
+        self.conv, self.wgrad = _load_section(self.path, section)  # this process's / the user's choices
         self.dirty = False
-        if self.path is not None and self.path.exists():
-            try:
-                data = json.loads(self.path.read_text())
-                sec = data.get("sections", {}).get(section, {}) if data.get("version") == VERSION else {}
-                self.conv = dict(sec.get("conv", {}))
-                self.wgrad = dict(sec.get("wgrad", {}))
-            except (OSError, ValueError):
-                self.conv, self.wgrad = {}, {}
 
     # conv: (config id, split-K factor / -stream-K grid)
     def get_conv(self, key) -> Optional[tuple]:
-        v = self.conv.get(_key(key))
+        k = _key(key)
+        v = self.sys_conv.get(k, self.conv.get(k))
         return (int(v[0]), int(v[1])) if v is not None else None
 
     def put_conv(self, key, val) -> None:
@@ -73,7 +89,8 @@ class TuneDB:
 
     # wgrad: (split target, pipeline, atomic, min steps)
     def get_wgrad(self, key) -> Optional[tuple]:
-        v = self.wgrad.get(_key(key))
+        k = _key(key)
+        v = self.sys_wgrad.get(k, self.wgrad.get(k))
         return (int(v[0]), int(v[1]), bool(v[2]), int(v[3])) if v is not None else None
 
     def put_wgrad(self, key, val) -> None:
@@ -81,11 +98,13 @@ class TuneDB:
         self.dirty = True
 
     def save(self) -> bool:
-        """Merge this section into the file (entries already on disk for this section are kept
-        unless this process has its own choice for the same key). Returns True if written."""
-        if self.path is None or not self.dirty:
+        """Merge this section into the user database (entries already on disk for this section
+        are kept unless this process has its own choice for the same key). The system database
+        is never written. Returns True if written."""
+        if self.path is None or not self.dirty or self.path.resolve() == SYSTEM_PATH.resolve():
             return False
         with _LOCK:
+            self.path.parent.mkdir(parents=True, exist_ok=True)
             data = {"version": VERSION, "sections": {}}
             if self.path.exists():
                 try:

@@ -53,7 +53,7 @@ def use_priority_main_stream():
     sharing one in-order queue with the executor's weight-gradient side stream -- no
     wgrad/dgrad overlap (one-GPU single-rank engine: 12.9-13.0 ms vs 11.3 ms per ResNet-50 step).
     Not for HIP-graph capture: a graph replayed from a high-priority stream measured 19.4 vs
-    11.2 ms. DRN_MAIN_PRIORITY=0 disables it. Returns the stream (None when disabled)."""
+    11.2 ms. Returns the stream (None without a GPU)."""
     s = make_priority_stream()
     if s is not None:
         s.wait_stream(torch.cuda.current_stream())
@@ -64,11 +64,10 @@ def use_priority_main_stream():
 def make_priority_stream():
     """The high-priority stream use_priority_main_stream() switches to, without switching: for a
     caller that runs only its eager steps on it (bench.py's auto mode, whose HIP-graph candidate
-    must stay on a normal-priority stream). None when DRN_MAIN_PRIORITY=0 or there is no GPU."""
-    prio = int(os.environ.get("DRN_MAIN_PRIORITY", "-1"))
-    if prio == 0 or not torch.cuda.is_available():
+    must stay on a normal-priority stream). None when there is no GPU."""
+    if not torch.cuda.is_available():
         return None
-    return torch.cuda.Stream(priority=prio)
+    return torch.cuda.Stream(priority=-1)
 
 
 def p2p_wanted(allreduce: str, grad_bytes: int, world: int, mode: str = "sync", shard_optimizer: bool = False,

@@ -154,7 +154,7 @@ class P2PAllReduce:
         dev = grad.device
         self.two_shot_min = 1024 * (two_shot_min_kb if two_shot_min_kb >= 0 else
                                     int(os.environ.get("DRN_P2P_TWO_SHOT_MIN_KB", "1024")))
-        self.wire = (wire or os.environ.get("DRN_P2P_WIRE", "fp32")).lower()
+        self.wire = (wire or "fp32").lower()
         if self.wire not in ("fp32", "bf16"):
             raise ValueError(f"P2P wire type must be fp32 or bf16, got {self.wire!r}")
         self.timeout_ms = int(os.environ.get("DRN_P2P_TIMEOUT_MS", "60000"))
@@ -302,7 +302,7 @@ class P2PAllReduce:
             # a collective until the process-group timeout; without the barrier the exported
             # buffers are left to process exit instead of being freed here
             try:
-                self._store_barrier(float(os.environ.get("DRN_P2P_CLOSE_TIMEOUT_S", "60")))
+                self._store_barrier(60.0)
             except Exception as e:  # noqa: BLE001 -- any failure: keep the buffers mapped
                 log.warning("P2P close: peers did not reach the teardown barrier (%s); buffers left to exit", e)
                 self._leaked, self._bufs = self._bufs, []   # (no release: a peer may still map them)

@@ -105,20 +105,15 @@ class Executor:
                  materialize_bn: Optional[bool] = None):
         self.spec, self.N, self.be = spec, batch, backend
         # fuse each BN's backward reduction into the epilogue of the data-gradient conv feeding it
-        self.fuse_bn_bwd = os.environ.get("DRN_FUSE_BN_BWD", "1") == "1"
-        # BN backward of the 3x3 conv's input fused into the 1x1 conv's weight / data gradients
-        # (BNB prologue: no materialised apply). Tested, but OFF by default: the 1x1 data
-        # gradient re-reads its narrow input once per output-channel tile (4-8x), so the extra
-        # BN-input DMA and the in-LDS transform cost more than the apply pass they replace
-        # (ResNet-50 bs128, scripts/op_breakdown.py: applies -330 us, consumers +800 us; step
-        # 10.74 -> 11.18 ms)
-        self.fuse_bnb = os.environ.get("DRN_FUSE_BNB", "0") == "1"
+        self.fuse_bn_bwd = True
+        # (The BN backward applied on load by both 1x1 consumers instead of materialised -- the
+        # "BNB prologue" -- measured slower: the 1x1 data gradient re-reads its narrow input once
+        # per output-channel tile, ResNet-50 bs128 10.74 -> 11.18 ms; removed in round 5.)
         # split-K weight gradients may accumulate with fp32 atomics (the autotuner's choice per
         # layer; the gradients are then zeroed at the start of every backward); not in the
         # bitwise-reproducible mode
         if hasattr(backend, "wgrad_atomic_ok"):
-            backend.wgrad_atomic_ok = os.environ.get("DRN_WGRAD_ATOMIC", "1") == "1" and \
-                os.environ.get("DRN_DETERMINISTIC", "0") != "1"
+            backend.wgrad_atomic_ok = os.environ.get("DRN_DETERMINISTIC", "0") != "1"
         # debug mode: synchronous finiteness checks after every block (forward and backward)
         self.check_nan = os.environ.get("DRN_CHECK_NAN", "0") == "1"
         # deterministic mode (DRN_DETERMINISTIC=1): bitwise-reproducible steps -- one statistics
@@ -132,14 +127,14 @@ class Executor:
         # (Producer-side finalize variants -- the last-arriving conv workgroup per channel column,
         # or the streaming apply kernels finalizing G == 1 statistics -- measured slower than the
         # consumer-side finalize below (ResNet-50: 12.85 vs 11.78 ms) and were removed.)
-        # Consumer-side BN finalize (DRN_CFIN, default on for HIP): no finalize launches at all --
+        # Consumer-side BN finalize (off only in the deterministic mode): no finalize launches --
         # the kernels CONSUMING a BatchNorm (the fused-prologue 1x1 convs, the materialising
         # apply, the backward apply) derive its parameters from the statistics replicas in their
         # own prologue and the first of them publishes them (ops/backend.py BnCfin). Removes ~98
         # dependent ~6 us launches per ResNet-50 step from the critical path.
-        self.cfin = not self.deterministic and os.environ.get("DRN_CFIN", "1") == "1"
+        self.cfin = not self.deterministic
         # single-phase strided data gradients zero the other phases in their own epilogue
-        self.out_fill = os.environ.get("DRN_OUT_FILL", "1") == "1"
+        self.out_fill = True
         self.device = torch.device(device)
         self.wd, self.mom = weight_decay, momentum
         self.is_hip = backend.name == "hip"
@@ -151,10 +146,11 @@ class Executor:
         # (Forking the projection-shortcut forward conv onto this stream measured neutral, and a
         # CU-masked side stream +0-0.4 %; both were removed.)
         self.side = None
-        # the data-gradient weight refresh after each update on the side stream (eager steps)
-        self.tflip_side = os.environ.get("DRN_TFLIP_SIDE", "1") == "1"
+        # the data-gradient weight refresh after each update on the side stream (eager steps;
+        # neutral vs the main stream, profiles/r4_tflip_side_ab.txt)
+        self.tflip_side = True
         # gradient-buffer claims skip the cross-queue wait when the reader already finished
-        self.claim_query = os.environ.get("DRN_CLAIM_QUERY", "1") == "1"
+        self.claim_query = True
         if self.is_hip and os.environ.get("DRN_WGRAD_STREAM", "1") == "1":
             self.side = torch.cuda.Stream(self.device)
         # gradient-buffer reuse guard: id(buffer) -> sequence number of the side-stream weight
@@ -168,7 +164,7 @@ class Executor:
         # gradients AFTER the buffer's reader (still many blocks old, so normally complete when
         # the main stream gets there): it covers the next claims too -- one cross-queue barrier
         # packet per claim_span claims instead of one per data gradient
-        self.claim_span = int(os.environ.get("DRN_CLAIM_SPAN", "12"))
+        self.claim_span = 12  # profiles/r4_claim_span_ab.txt
         # BN-apply+ReLU either fused into every consuming conv's load prologue (recomputed by the
         # forward conv, the projection conv and both weight-gradient convs; the LDS-DMA kernels
         # rewrite each landed stage in LDS before its barrier) or materialised once per BN by a
@@ -190,13 +186,13 @@ class Executor:
         # 512->2048: 4-16 tiles) spend more VALU on it than one streaming apply pass costs
         # (ResNet-50 bs128, same box, with the 3M threshold below: tiles 8 10.25-10.31 ms, 16
         # 10.29-10.31, 4 10.38-10.40, off 10.36-10.37 -- profiles/r2_experiments.md)
-        self.mat_tiles = int(os.environ.get("DRN_BN_MAT_TILES", "8"))
+        self.mat_tiles = 8
         # ... but only BN tensors of >= DRN_BN_MAT_MIN_ELEMS elements: below that a step is
         # launch-latency bound and the extra streaming launch costs more than the 3x3 consumer's
         # in-LDS rewrite (CIFAR ResNet-50 bs 128: 2.45 ms materialised vs 2.33 ms fused; its
         # largest BN input is 128x32x32x16 = 2.1M). 3M: the ImageNet 7x7x512 stage (3.2M at bs128)
         # is materialised -- its 3x3 conv and weight gradient ran 80 / 77 us with the prologue
-        self.mat_min_elems = int(os.environ.get("DRN_BN_MAT_MIN_ELEMS", "3000000"))
+        self.mat_min_elems = 3_000_000
         self.fdt = backend.acc_dtype
         self.P = params or ParamStore(spec, self.device, keep_bf16=self.is_hip, seed=seed, dtype=self.fdt)
         self.grad_ready: Optional[Callable[[int], None]] = None
@@ -331,14 +327,14 @@ class Executor:
         self._tflip_ev = None  # side stream: the data-gradient weights of the next backward are ready
         img = sp.image_size
         self.images = self._act(N, img, img, sp.stem.cin_store)
-        # Packed stem (csrc/kernels/stem.hip, DRN_STEM_PACK=1 default on HIP): the 7x7/2 stem over
+        # Packed stem (csrc/kernels/stem.hip, on the HIP backend): the 7x7/2 stem over
         # RGB runs on a 4-channel copy of the images with a zero pixel column on each side and on
         # weights padded to 8 taps per row, so one 16-byte piece is a tap PAIR: 4 forward k-stages
         # instead of 7 and 2 weight-gradient k-tiles instead of 4 (62.5 % of the 8-channel
         # reduction is zero padding). Checkpoint / optimizer layout is unchanged: the packed
         # weights are derived after every update, the gradient mapped back after the wgrad.
         c0 = sp.stem
-        self.stem_pack = (self.is_hip and os.environ.get("DRN_STEM_PACK", "1") == "1" and c0.k % 2 == 1
+        self.stem_pack = (self.is_hip and c0.k % 2 == 1
                           and c0.stride == 2 and c0.cin <= 4 and c0.cin_store == 8 and img % 2 == 0)
         if self.stem_pack:
             s8 = c0.k + 1
@@ -459,11 +455,8 @@ class Executor:
         # point its data exists whatever the pool size; the pool only decides how long the
         # critical-path data gradients wait for side-stream readers (single-rank RCCL engine,
         # ResNet-50 bs128: 10.02 ms vs 9.87 ms plain, profiles/r4_base).
-        nbuf_env = os.environ.get("DRN_GRAD_BUFS")
         buf_bytes = max_act * torch.finfo(self.be.act_dtype).bits // 8
-        if nbuf_env is not None:
-            nbuf = max(3, int(nbuf_env))
-        elif self.side is not None and buf_bytes >= (64 << 20):
+        if self.side is not None and buf_bytes >= (64 << 20):
             cap = int(0.08 * torch.cuda.get_device_properties(self.device).total_memory) // max(1, buf_bytes) \
                 if self.device.type == "cuda" else 32
             nbuf = max(6, min(32, cap))
@@ -740,18 +733,18 @@ class Executor:
             self.grad_ready(lo)
 
     # -- weight gradients on the side stream ---------------------------------------------------------
-    def _wgrad(self, x, dy, dw, geom, in_bn=None, dy_buf=None, bnb=None, post=None):
+    def _wgrad(self, x, dy, dw, geom, in_bn=None, dy_buf=None, post=None):
         """Weight gradient into dw (on the side stream when enabled); post() runs right after it,
         on the same stream (the packed stem maps its gradient back to the checkpoint layout)."""
         if self.side is None:
-            self.be.conv_wgrad(x, dy, dw, geom, in_bn=in_bn, ws=self.wgrad_ws, bnb=bnb)
+            self.be.conv_wgrad(x, dy, dw, geom, in_bn=in_bn, ws=self.wgrad_ws)
             if post is not None:
                 post()
             return
         main = torch.cuda.current_stream(self.device)
         self.side.wait_stream(main)                      # x and dy are complete
         with torch.cuda.stream(self.side):
-            self.be.conv_wgrad(x, dy, dw, geom, in_bn=in_bn, ws=self.wgrad_ws, bnb=bnb)
+            self.be.conv_wgrad(x, dy, dw, geom, in_bn=in_bn, ws=self.wgrad_ws)
             if post is not None:
                 post()
         if dy_buf is not None:                           # the main stream must not overwrite dy early
@@ -794,7 +787,7 @@ class Executor:
         else:
             main.wait_event(ev)
 
-    def _dgrad(self, op: ConvOp, dy, dx, accumulate: bool, bn: Optional[BNState] = None, bn_x=None, bnb=None):
+    def _dgrad(self, op: ConvOp, dy, dx, accumulate: bool, bn: Optional[BNState] = None, bn_x=None):
         """Data gradient of `op` into dx (+= when accumulate). With bn set (requires a launch set
         covering every dx element) the epilogue also performs that BN's backward reduction."""
         # a single-phase strided data gradient (1x1 stride-2 projection) writes the zeros of the
@@ -809,7 +802,7 @@ class Executor:
             fuse = (bn_x, bn.scale, bn.shift, bn.mean, bn.invstd)
         for ph in op.dg:
             self.be.conv_fwd(dy, ph.wt, dx, ph.geom, residual=dx if accumulate else None, out_map=ph.out_map,
-                             stats=bn.bacc if fuse is not None else None, bn_bwd=fuse, out_fill=fill, bnb=bnb)
+                             stats=bn.bacc if fuse is not None else None, bn_bwd=fuse, out_fill=fill)
 
     def _block_bwd(self, bp: BlockPlan, bufs, cur: int) -> int:
         """Back-propagates one block; bufs[cur] holds d(block output). Returns the index of the
@@ -821,13 +814,12 @@ class Executor:
         d_out = self._view(bufs[cur], bp.out)
         ins = [bp.x] + bp.hs                 # raw inputs of each main-path conv
         dy, dy_buf, dy_k = d_out, bufs[cur], cur
-        lazy = None  # (bn input, BnCfin): dy is the masked gradient g of a non-materialised BN backward
         for i in reversed(range(len(bp.convs))):
             op, xin, b = bp.convs[i], ins[i], bp.bn[i]
             tgt_k = self._take(bufs, (cur, dy_k))
             tgt = bufs[tgt_k]
             a_in, pro = (b.act, None) if b.act is not None else (b.src, b.ss)
-            self._wgrad(a_in, dy, op.dw, op.geom, in_bn=pro, dy_buf=dy_buf, bnb=lazy)
+            self._wgrad(a_in, dy, op.dw, op.geom, in_bn=pro, dy_buf=dy_buf)
             if i == 0 and bp.proj is not None:
                 self._wgrad(a_in, d_out, bp.proj.dw, bp.proj.geom, in_bn=pro, dy_buf=bufs[cur])
             self._claim(tgt)
@@ -839,32 +831,14 @@ class Executor:
                 # that its (full-cover, stride-1) epilogue can carry the fused BN reduction
                 pj = bp.proj
                 self._dgrad(pj, d_out, da, accumulate=False)
-                self._dgrad(op, dy, da, accumulate=True, bn=b if fuse else None, bn_x=xin, bnb=lazy)
+                self._dgrad(op, dy, da, accumulate=True, bn=b if fuse else None, bn_x=xin)
             else:
-                self._dgrad(op, dy, da, accumulate=False, bn=b if fuse else None, bn_x=xin, bnb=lazy)
+                self._dgrad(op, dy, da, accumulate=False, bn=b if fuse else None, bn_x=xin)
                 if i == 0:
                     add = d_out              # identity shortcut
-            lazy = None
-            if fuse and self._bnb_ok(bp, i, xin):
-                # the BN backward of conv i's input is not materialised: both consumers (the
-                # previous conv's weight and data gradients, 1x1) apply it to g on load
-                lazy = (xin, BnCfin(b.bacc, float(xin.numel() // b.bn.c), b.gamma, mean=b.mean, invstd=b.invstd,
-                                    dgamma=b.dgamma, dbeta=b.dbeta, publish=True))
-            else:
-                self._bn_bwd(b, xin, da, da, add=add, reduced=fuse)
+            self._bn_bwd(b, xin, da, da, add=add, reduced=fuse)
             dy, dy_buf, dy_k = da, tgt, tgt_k
         return dy_k
-
-    def _bnb_ok(self, bp: BlockPlan, i: int, xin) -> bool:
-        """Whether the BN backward feeding conv i-1 can be fused into that conv's consumers:
-        interior BN (i >= 1, no residual add), consumer a 1x1 stride-1 conv whose data gradient is
-        one full-cover launch, channels on the LDS-DMA path (C % 64 == 0), consumer-side
-        finalize mode (DRN_FUSE_BNB=0 keeps the materialised apply)."""
-        if not self.fuse_bnb or i < 1 or not self.cfin:
-            return False
-        prev = bp.convs[i - 1]
-        return prev.conv.k == 1 and prev.conv.stride == 1 and prev.full_cover and len(prev.dg) == 1 \
-            and xin.shape[-1] % 64 == 0
 
     def _take(self, bufs, busy) -> int:
         """Index of the least recently used gradient buffer not holding a live gradient (`busy`);
@@ -959,8 +933,7 @@ class Executor:
         self.P.grad.zero_()
         if self.is_hip:
             torch.cuda.synchronize()
-            if os.environ.get("DRN_INSITU_TUNE", "1") == "1":
-                self.insitu_tune(rounds=int(os.environ.get("DRN_INSITU_ROUNDS", "2")))
+            self.insitu_tune(rounds=int(os.environ.get("DRN_INSITU_ROUNDS", "2")))
             if hasattr(self.be, "save_tune_db"):
                 self.be.save_tune_db()   # persist newly timed kernel choices (ops/tunedb.py)
 

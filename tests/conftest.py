@@ -1,5 +1,6 @@
 import os
 import sys
+import tempfile
 
 import pytest
 
@@ -9,6 +10,9 @@ if REPO not in sys.path:
 
 
 def pytest_configure(config):
+    # kernel choices the tests tune go to a throw-away user database: neither the shipped system
+    # database (read-only anyway) nor the user's ~/.cache one sees per-test quick tunings
+    os.environ.setdefault("DRN_TUNE_DB", os.path.join(tempfile.mkdtemp(prefix="drn-tune-"), "tune_db.json"))
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and the in-tree HIP kernel library")
     config.addinivalue_line("markers", "slow: long-running integration test")
 

@@ -77,11 +77,3 @@ def test_sgd_step_matches_torch_momentum():
     m = g * 0.5 + 2e-4 * w0
     assert torch.allclose(ex.P.master, w0 - 0.1 * m, atol=1e-6)
     assert torch.allclose(ex.P.momentum, m, atol=1e-6)
-
-
-def test_imagenet_resnet50_fp64_fused_bn_backward(monkeypatch):
-    """The non-materialised BN backward (DRN_FUSE_BNB=1: dY = A*g + B*x + D applied by the 1x1
-    consumers' weight and data gradients, dgamma / dbeta published by the data gradient) gives
-    the oracle's gradients."""
-    monkeypatch.setenv("DRN_FUSE_BNB", "1")
-    _check(imagenet_resnet_v2(50, num_classes=7, image_size=64), 2, torch.float64, 1e-9)

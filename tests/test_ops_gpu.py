@@ -949,83 +949,6 @@ def _prologue_finalize_case(hip, publish, N, H, C, K):
         assert bool((sc == 7.0).all())
 
 
-def _bnb_case(N, H, C, seed):
-    """(g, x, BnCfin on both devices, dy_eff reference) of a non-materialised BN backward."""
-    from distributed_resnet_tensorflow_amd.ops.backend import BnCfin
-    torch.manual_seed(seed)
-    g = bf(torch.randn(N, H, H, C))
-    x = bf(torch.randn(N, H, H, C))
-    G = 3
-    stats = torch.randn(G, 2, C) * 50.0
-    gamma, mean, istd = torch.rand(C) + 0.5, torch.randn(C) * 0.2, torch.rand(C) + 0.5
-    cnt = float(N * H * H)
-    p = stats.double().sum(0)
-    xh = (x.double() - mean.double()) * istd.double()
-    ref = (gamma * istd).double() * (g.double() - p[0] / cnt - xh * (p[1] / cnt))
-    dg, db = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
-    f = BnCfin(stats.cuda(), cnt, gamma.cuda(), mean=mean.cuda(), invstd=istd.cuda(), dgamma=dg, dbeta=db,
-               publish=True)
-    return g, x, f, ref.float(), p
-
-
-@pytest.mark.parametrize("cfg", [0, 3, 6, 13, 12])
-@pytest.mark.parametrize("epi", ["plain", "bn_bwd", "bn_bwd_acc"])
-def test_conv_bnb_prologue(hip, ref, cfg, epi):
-    """1x1 data-gradient conv whose input is dx of a NON-materialised BN backward: the LDS-DMA
-    kernel applies A*g + B*x + D to each landed stage (BNB prologue), publishes dgamma / dbeta,
-    and still runs its own fused BN-backward epilogue / accumulation."""
-    N, H, C, K = 2, 11, 128, 64          # M = 242: partial pixel tiles
-    g, x, f, dy_ref, p = _bnb_case(N, H, C, 21 + cfg)
-    wt = bf(torch.randn(K, 1, 1, C) * 0.05)
-    geo = ConvGeom(1, 0, 0)
-    kw_ref, kw_hip = {}, {}
-    y0 = torch.zeros(N, H, H, K)
-    if epi != "plain":
-        xb = bf(torch.randn(N, H, H, K))
-        sc, sh = torch.rand(K) + 0.5, torch.randn(K) * 0.3
-        mu, isd = torch.randn(K) * 0.1, torch.rand(K) + 0.5
-        st_ref = torch.zeros(2 * K)
-        kw_ref = dict(stats=st_ref, bn_bwd=(xb.float(), sc, sh, mu, isd))
-        st = torch.zeros(2, K, device="cuda")
-        kw_hip = dict(stats=st, bn_bwd=(xb.cuda(), sc.cuda(), sh.cuda(), mu.cuda(), isd.cuda()))
-        if epi == "bn_bwd_acc":
-            y0 = bf(torch.randn(N, H, H, K)).float()
-    y_ref = y0.clone()
-    ref.conv_fwd(bf(dy_ref).float(), wt.float(), y_ref, geo, residual=y0 if epi == "bn_bwd_acc" else None, **kw_ref)
-    y = y0.to(torch.bfloat16).cuda()
-    a = hip.conv_args(g.cuda(), wt.cuda(), y, geo, residual=y if epi == "bn_bwd_acc" else None,
-                      bnb=(x.cuda(), f), **kw_hip)
-    a.cfg = cfg
-    hip.launch_conv(a)
-    torch.cuda.synchronize()
-    assert rel(y, y_ref) < 2e-2, cfg
-    if epi != "plain":
-        s_hip = kw_hip["stats"].view(-1).cpu()
-        assert rel(s_hip[:K], kw_ref["stats"][:K]) < 3e-2
-        assert rel(s_hip[K:], kw_ref["stats"][K:]) < 3e-2
-    assert rel(f.dbeta, p[0].float()) < 1e-5 and rel(f.dgamma, p[1].float()) < 1e-5
-
-
-@pytest.mark.parametrize("ns", [2, 3, 4, 5, 6, 7, 8])
-@pytest.mark.parametrize("pro", [False, True])
-def test_wgrad_bnb_prologue(hip, ref, ns, pro):
-    """1x1 weight gradient whose dY is dx of a non-materialised BN backward (BNB on the dY
-    image), optionally with the fused forward-BN prologue on the x image too."""
-    N, H, C, K = 2, 13, 64, 128          # K = channels of dY
-    g, xb, f, dy_ref, _ = _bnb_case(N, H, K, 5 + ns)
-    x = bf(torch.randn(N, H, H, C))
-    in_bn = (torch.rand(C) + 0.5, torch.randn(C) * 0.3) if pro else None
-    dw_ref = torch.zeros(K, 1, 1, C)
-    ref.conv_wgrad(x.float(), bf(dy_ref).float(), dw_ref, ConvGeom(1, 0, 0), in_bn=in_bn)
-    dw = torch.zeros(K, 1, 1, C, device="cuda")
-    ws = torch.zeros(max(16, hip.wgrad_ws_elems(N * H * H, K, 1, 1, C)), device="cuda")
-    a = hip.wgrad_args(x.cuda(), g.cuda(), dw, ConvGeom(1, 0, 0), in_bn=None if in_bn is None else
-                       (in_bn[0].cuda(), in_bn[1].cuda()), ws=ws, bnb=(xb.cuda(), f))
-    hip._wgrad_full(a, ns, dw, hip.stream())
-    torch.cuda.synchronize()
-    assert rel(dw, dw_ref) < 2e-2, ns
-
-
 @pytest.mark.parametrize("case", [(4, 16, 16, 16, 3, 1, 1), (4, 24, 64, 32, 1, 1, 0), (4, 33, 32, 64, 3, 2, 1)])
 @pytest.mark.parametrize("ns", [0, 2, 5, 7])
 def test_wgrad_atomic_split_k(hip, ref, case, ns):

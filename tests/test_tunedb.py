@@ -82,6 +82,33 @@ def test_shipped_database_matches_the_tree():
     """The shipped database's section is keyed by the current tuning-source hash, so a bench run
     on an MI355X uses it instead of re-tuning."""
     from distributed_resnet_tensorflow_amd.ops import build
-    from distributed_resnet_tensorflow_amd.ops.tunedb import DEFAULT_PATH
-    secs = json.loads(DEFAULT_PATH.read_text())["sections"]
+    from distributed_resnet_tensorflow_amd.ops.tunedb import SYSTEM_PATH
+    secs = json.loads(SYSTEM_PATH.read_text())["sections"]
     assert any(s.endswith("|" + build.tune_hash()[:16]) for s in secs), list(secs)
+
+
+def test_system_database_is_read_only_and_read_first(tmp_path, monkeypatch):
+    """The shipped (system) database is consulted before the user database and never written:
+    a run's own quick tunings land in the user file only (a test run must not
+    replace the shipped MI355X choices)."""
+    sysdb, user = tmp_path / "system.json", tmp_path / "user.json"
+    s = TuneDB("gfx950/256cu|abcd", sysdb)
+    s.put_conv((1, 2), (7, 1))
+    s.put_wgrad((3,), (512, 2, False, 8))
+    assert s.save()
+    before = sysdb.read_text()
+    u = TuneDB("gfx950/256cu|abcd", user, system=sysdb)
+    assert u.get_conv((1, 2)) == (7, 1) and u.get_wgrad((3,)) == (512, 2, False, 8)
+    u.put_conv((1, 2), (9, 1))              # a quick re-tune of a shipped geometry...
+    u.put_conv((5, 6), (4, 1))
+    assert u.save()
+    assert sysdb.read_text() == before      # ...never touches the system file
+    again = TuneDB("gfx950/256cu|abcd", user, system=sysdb)
+    assert again.get_conv((1, 2)) == (7, 1)  # the system choice wins
+    assert again.get_conv((5, 6)) == (4, 1)  # the user file fills the gaps
+    monkeypatch.setenv("DRN_TUNE_DB", str(sysdb))
+    from distributed_resnet_tensorflow_amd.ops import tunedb
+    monkeypatch.setattr(tunedb, "SYSTEM_PATH", sysdb)
+    w = TuneDB("gfx950/256cu|abcd")         # pointed at the system file: writes are refused
+    w.put_conv((8,), (1, 1))
+    assert not w.save() and sysdb.read_text() == before
