@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--width", type=int, default=1, help="bottleneck width multiplier (2 = Wide-ResNet-50-2)")
     ap.add_argument("--batch_size", type=int, default=128, help="per-GPU batch")
     ap.add_argument("--graph", type=int, default=-1, help="capture the step in a HIP graph (-1: auto)")
+    ap.add_argument("--plan", type=int, default=-1,
+                    help="native step plan (runtime/plan.py): -1 auto (timed against the other modes), 0 off, 1 force")
     ap.add_argument("--bucket_mb", type=float, default=25.0)
     ap.add_argument("--allreduce", default="auto", choices=["rccl", "p2p", "auto"],
                     help="auto: the one-shot P2P kernel when the whole gradient is <= 64 MB (CIFAR), else RCCL")
@@ -98,6 +100,9 @@ def main():
         from distributed_resnet_tensorflow_amd.parallel.engine import make_priority_stream
         prio = make_priority_stream()
     if world > 1 or force_dp:
+        # per-collective device timing (two events per bucket all-reduce): the JSON line then
+        # reports the exchange's total time and its overlap with the backward pass
+        os.environ.setdefault("TORCH_NCCL_ENABLE_TIMING", "1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -106,6 +111,7 @@ def main():
     from distributed_resnet_tensorflow_amd.ops.backend import HipBackend
     from distributed_resnet_tensorflow_amd.runtime.executor import Executor
     from distributed_resnet_tensorflow_amd.runtime.graph import SegmentedStepGraph, StepGraph
+    from distributed_resnet_tensorflow_amd.runtime.plan import StepPlan
     from distributed_resnet_tensorflow_amd.parallel.engine import DataParallelEngine
 
     be = HipBackend("cuda")
@@ -147,62 +153,93 @@ def main():
     # the ~20 graph launches cost more than the host-side kernel launches they replace
     # (the P2P all-reduce is a set of kernels with device-side flags: a data-parallel step on it is
     # captured whole, comm included -- SURVEY §5.8)
+    def _time(fn, n=5):
+        fn()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t
+
+    def _agree(ts):
+        """Every rank takes the same decision: the slowest rank's timings."""
+        if world > 1:
+            tt = torch.tensor(ts, dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            ts = tt.tolist()
+        return ts
+
+    def _pick(cands):
+        """{name: fn} -> the fastest (best of 3 interleaved rounds of 5 untimed-for-the-result
+        steps each: a single 5-step comparison picked a slower mode once in three runs)."""
+        names = list(cands)
+        best = [float("inf")] * len(names)
+        for _ in range(3):
+            for i, k in enumerate(names):
+                best[i] = min(best[i], _time(cands[k]))
+        best = _agree(best)
+        i = min(range(len(names)), key=lambda j: best[j])
+        return names[i], {k: round(v / 5 * 1e3, 3) for k, v in zip(names, best)}
+
+    # Step modes (every one runs the same kernels on the same buffers; the choice changes the
+    # step time, not the numerics):
+    #   eager  -- the Python step, critical path on a high-priority stream;
+    #   plan   -- the eager step recorded once and replayed from C++ (runtime/plan.py): same
+    #             streams and priorities, a few host calls per step instead of ~340 launches;
+    #   graph  -- the whole step as one HIP graph (P2P data parallelism included), optionally
+    #             without the weight-gradient side stream (one-stream graph);
+    #   segmented -- RCCL data parallelism as a chain of graphs (--graph 1).
     use_graph = args.graph if args.graph >= 0 else int(eng is None or eng.p2p is not None)
-    run = step
     if eng is not None and eng.zero1:
         use_graph = 0
+    want_plan = args.plan != 0 and (eng is None or (eng.p2p is None and not eng.zero1 and eng.mode == "sync"))
+    cands, mode_times = {}, None
+
+    def in_eager_ctx(fn):
+        if prio is None:
+            return fn
+        def f():
+            with torch.cuda.stream(prio):
+                fn()
+        return f
+
     if use_graph and eng is not None and eng.p2p is None:
-        sg = SegmentedStepGraph(ex, eng, 1.0 / world, warmup=1)
-        run = sg.replay
+        cands["segmented"] = SegmentedStepGraph(ex, eng, 1.0 / world, warmup=1).replay
     elif use_graph:
         sg = StepGraph(step, warmup=2)
-        run = sg.replay
-        if args.graph == -1:
-            # auto: keep whichever of graph replay and eager launches is faster for this step
-            # (untimed, before the warm-up). Short steps (CIFAR, 2.8 ms) are host-launch-bound
-            # eager (5.3 ms); the ResNet-50 ImageNet step measured faster eager (10.55 vs 10.85
-            # ms): the host stays ahead and the replay adds gaps around the side-stream branches
-            def _time(fn, n=5):
-                fn()
-                torch.cuda.synchronize()
-                t = time.perf_counter()
-                for _ in range(n):
-                    fn()
-                torch.cuda.synchronize()
-                return time.perf_counter() - t
-
-            # (best of 3 interleaved rounds: a single 5-step comparison picked the graph for
-            # ResNet-50 once in three runs at 10.34 ms vs 10.06 eager, profiles/r2_bench_s19.jsonl)
-            t_eager, t_graph = float("inf"), float("inf")
-            for _ in range(3):
-                t_eager = min(t_eager, _time(eager))
-                t_graph = min(t_graph, _time(sg.replay))
-            if world > 1:
-                # every rank takes the same decision (the slowest rank's timings)
-                tt = torch.tensor([t_eager, t_graph], dtype=torch.float64,
-                                  device="cuda" if backend == "nccl" else "cpu")
-                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-                t_eager, t_graph = tt.tolist()
-            if t_eager < t_graph:
-                run, use_graph = eager, 0
-            elif (eng is None or eng.p2p is not None) and ex.side is not None:
-                # the graph candidate without the weight-gradient side stream (one stream: CIFAR
-                # ResNet-50 bs32 1.585 vs 1.785 ms; the side stream wins for larger steps)
-                side, ex.side = ex.side, None
-                sg1 = StepGraph(step, warmup=2)
-                t_one = float("inf")
-                for _ in range(3):
-                    t_one = min(t_one, _time(sg1.replay))
-                if world > 1:  # every rank takes the same decision (the slowest rank's timings)
-                    tt = torch.tensor([t_one, t_graph], dtype=torch.float64,
-                                      device="cuda" if backend == "nccl" else "cpu")
-                    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-                    t_one, t_graph = tt.tolist()
-                if t_one < t_graph:
-                    run = sg1.replay
-                else:
-                    ex.side = side
-                    del sg1
+        cands["graph"] = sg.replay
+    if args.graph != 1 or not cands:
+        cands["eager"] = eager
+    if want_plan and (args.plan == 1 or "eager" in cands):
+        with torch.cuda.stream(prio) if prio is not None else torch.cuda.stream(torch.cuda.current_stream()):
+            plan = StepPlan(ex, eng, grad_scale=1.0 / world, warmup=1)
+        cands["plan"] = in_eager_ctx(plan.replay)
+        if args.plan == 1:
+            cands.pop("eager", None)
+    mode = next(iter(cands))
+    if len(cands) > 1:
+        mode, mode_times = _pick(cands)
+    if mode == "graph" and (eng is None or eng.p2p is not None) and ex.side is not None and args.graph == -1:
+        # the graph candidate without the weight-gradient side stream (one stream: CIFAR
+        # ResNet-50 bs32 1.585 vs 1.785 ms; the side stream wins for larger steps)
+        side, ex.side = ex.side, None
+        sg1 = StepGraph(step, warmup=2)
+        m1, t1 = _pick({"graph": cands["graph"], "graph_one_stream": sg1.replay})
+        if m1 == "graph":
+            ex.side = side
+            del sg1
+        else:
+            cands["graph_one_stream"], mode = sg1.replay, m1
+        mode_times = {**(mode_times or {}), **t1}
+    run = cands[mode]
+    use_graph = int(mode in ("graph", "graph_one_stream", "segmented"))
+    # host enqueue time of one step of the chosen mode (from an idle queue: nothing blocks)
+    torch.cuda.synchronize()
+    t_host = time.perf_counter()
+    run()
+    t_host = (time.perf_counter() - t_host) * 1e3
+    torch.cuda.synchronize()
     for _ in range(args.warmup):
         run()
     torch.cuda.synchronize()
@@ -224,6 +261,18 @@ def main():
     ms = dt / args.steps * 1e3
     img_s = args.batch_size * world * args.steps / dt
     loss = float(ex.loss_vec.float().mean())
+    dp = None
+    if eng is not None:
+        # data-parallel diagnostics of the last timed step (rank 0's view; comm_exposed_ms = the
+        # exchange time left after the backward pass, overlap_fraction = the share of the
+        # collectives' device time hidden under it)
+        st = eng.stats()
+        dp = {"rccl_world": dist.get_world_size(), "backend": dist.get_backend(),
+              "allreduce": "p2p" if eng.p2p is not None else "rccl", "buckets": st.get("allreduce_buckets"),
+              "bucket_mb": args.bucket_mb, "wire": eng.wire}
+        for k in ("backward_ms", "comm_exposed_ms", "comm_ms", "overlap_fraction"):
+            if k in st:
+                dp[k] = round(float(st[k]), 3)
     if rank == 0:
         base = BASELINE_IMG_S.get(args.dataset, {}).get(world) if (args.width == 1 and args.resnet_size == 50) else None
         model = f"resnet{args.resnet_size}_v2_{args.dataset}" if args.dataset == "imagenet" else \
@@ -248,10 +297,15 @@ def main():
             "data": "synthetic (random-init weights, fixed synthetic batch of the benchmark shape)",
             "config": {"model": model, "global_batch": args.batch_size * world, "per_gpu_batch": args.batch_size,
                        "image_size": spec.image_size, "num_classes": spec.num_classes,
-                       "parallelism": f"dp{world}", "hip_graph": bool(use_graph),
+                       "parallelism": f"dp{world}", "hip_graph": bool(use_graph), "step_mode": mode,
                        "wgrad_side_stream": ex.side is not None},
             "final_loss": round(loss, 4),
+            "host_enqueue_ms": round(t_host, 3),
         }
+        if mode_times is not None:
+            out["mode_trial_ms"] = mode_times
+        if dp is not None:
+            out["data_parallel"] = dp
         print(json.dumps(out), file=result_out, flush=True)
     if os.environ.get("DRN_PRINT_TUNE") == "1" and rank == 0:
         for key, cfg, us in be.tune_log:

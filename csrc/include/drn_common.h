@@ -12,6 +12,10 @@
 
 #define DRN_API extern "C" __attribute__((visibility("default")))
 
+#include <tuple>
+#include <type_traits>
+#include <utility>
+
 typedef uint16_t bf16_t;
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short s16x8_t __attribute__((ext_vector_type(8)));
@@ -152,6 +156,38 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int q = nwg >> 3, r = nwg & 7;
   const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
   return base + (bid >> 3);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Kernel launch + native step plans (csrc/kernels/plan.hip). Every kernel of the library is
+// launched through drn::launch: normally a plain hipLaunchKernelGGL; while the CALLING thread
+// records a step plan, the launch (kernel, grid, block, LDS bytes, stream and a by-value copy of
+// every argument) is appended to the plan instead, to be replayed later by drn_plan_replay with
+// one host call per plan segment (no Python, no argument marshalling per launch).
+// ---------------------------------------------------------------------------------------------
+struct Plan;
+extern thread_local Plan* g_plan_rec;
+void plan_add_launch(Plan* p, const void* fn, dim3 grid, dim3 block, size_t shm, hipStream_t s, void* blob,
+                     void** argv, void (*del)(void*));
+
+template <typename T, size_t... I>
+inline void plan_argv(T* t, void** argv, std::index_sequence<I...>) {
+  ((argv[I] = static_cast<void*>(&std::get<I>(*t))), ...);
+}
+
+template <typename... KArgs, typename... Args>
+inline void launch(void (*kern)(KArgs...), dim3 grid, dim3 block, size_t shm, hipStream_t s, Args&&... args) {
+  static_assert(sizeof...(KArgs) == sizeof...(Args), "kernel argument count");
+  if (g_plan_rec != nullptr) {
+    using T = std::tuple<std::remove_cv_t<std::remove_reference_t<KArgs>>...>;
+    T* t = new T(std::forward<Args>(args)...);  // converted to the kernel's parameter types
+    void** argv = new void*[sizeof...(KArgs) + 1];
+    plan_argv(t, argv, std::index_sequence_for<KArgs...>{});
+    plan_add_launch(g_plan_rec, reinterpret_cast<const void*>(kern), grid, block, shm, s, t, argv,
+                    [](void* q) { delete static_cast<T*>(q); });
+    return;
+  }
+  hipLaunchKernelGGL(kern, grid, block, shm, s, std::forward<Args>(args)...);
 }
 
 }  // namespace drn

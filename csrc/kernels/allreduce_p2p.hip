@@ -222,7 +222,7 @@ static bool p2p_check(const drn::P2PArgs* a) {
 
 DRN_API int drn_p2p_signal(const drn::P2PArgs* a, int kind, hipStream_t s) {
   if (!p2p_check(a) || kind < 0 || kind >= drn::P2P_KINDS) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(drn::p2p_signal_kernel, dim3(1), dim3(64), 0, s, *a, kind);
+  drn::launch(drn::p2p_signal_kernel, dim3(1), dim3(64), 0, s, *a, kind);
   return (int)hipGetLastError();
 }
 
@@ -232,9 +232,9 @@ DRN_API int drn_p2p_reduce(const drn::P2PArgs* a, int blocks, int wire_bf16, hip
   if (!p2p_check(a)) return (int)hipErrorInvalidValue;
   if (blocks < 1) blocks = 1;
   if (wire_bf16)
-    hipLaunchKernelGGL(drn::p2p_reduce_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, *a);
+    drn::launch(drn::p2p_reduce_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, *a);
   else
-    hipLaunchKernelGGL(drn::p2p_reduce_kernel<float>, dim3(blocks), dim3(256), 0, s, *a);
+    drn::launch(drn::p2p_reduce_kernel<float>, dim3(blocks), dim3(256), 0, s, *a);
   return (int)hipGetLastError();
 }
 
@@ -244,17 +244,17 @@ DRN_API int drn_p2p_reduce2(const drn::P2PArgs* a, int blocks, int wire_bf16, hi
   if (!p2p_check(a)) return (int)hipErrorInvalidValue;
   if (blocks < 1) blocks = 1;
   if (wire_bf16)
-    hipLaunchKernelGGL(drn::p2p_rs_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, *a);
+    drn::launch(drn::p2p_rs_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, *a);
   else
-    hipLaunchKernelGGL(drn::p2p_rs_kernel<float>, dim3(blocks), dim3(256), 0, s, *a);
-  hipLaunchKernelGGL(drn::p2p_signal_kernel, dim3(1), dim3(64), 0, s, *a, (int)drn::P2P_RS_DONE);
-  hipLaunchKernelGGL(drn::p2p_ag_kernel, dim3(blocks), dim3(256), 0, s, *a);
+    drn::launch(drn::p2p_rs_kernel<float>, dim3(blocks), dim3(256), 0, s, *a);
+  drn::launch(drn::p2p_signal_kernel, dim3(1), dim3(64), 0, s, *a, (int)drn::P2P_RS_DONE);
+  drn::launch(drn::p2p_ag_kernel, dim3(blocks), dim3(256), 0, s, *a);
   return (int)hipGetLastError();
 }
 
 DRN_API int drn_p2p_step(const drn::P2PArgs* a, unsigned* epoch_rw, hipStream_t s) {
   if (!p2p_check(a)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(drn::p2p_step_kernel, dim3(1), dim3(64), 0, s, *a, epoch_rw);
+  drn::launch(drn::p2p_step_kernel, dim3(1), dim3(64), 0, s, *a, epoch_rw);
   return (int)hipGetLastError();
 }
 
@@ -263,7 +263,7 @@ DRN_API int drn_p2p_cast(const float* x, void* y, int64_t n, hipStream_t s) {
   int64_t b = (n / 4 + 255) / 256;
   if (b > 1024) b = 1024;
   if (b < 1) b = 1;
-  hipLaunchKernelGGL(drn::p2p_cast_kernel, dim3((unsigned)b), dim3(256), 0, s, x, (bf16_t*)y, n / 4);
+  drn::launch(drn::p2p_cast_kernel, dim3((unsigned)b), dim3(256), 0, s, x, (bf16_t*)y, n / 4);
   return (int)hipGetLastError();
 }
 

@@ -120,14 +120,14 @@ __global__ void synthetic_images_kernel(bf16_t* __restrict__ out, int64_t npix, 
 DRN_API int drn_cifar_augment(const uint8_t* in, const int* params, void* out, int N, int H, int W, int pad,
                               hipStream_t s) {
   if (H * W > 2048) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(drn::cifar_augment_kernel, dim3(N), dim3(256), 0, s, in, params, (bf16_t*)out, H, W, pad);
+  drn::launch(drn::cifar_augment_kernel, dim3(N), dim3(256), 0, s, in, params, (bf16_t*)out, H, W, pad);
   return (int)hipGetLastError();
 }
 
 DRN_API int drn_vgg_preprocess(const uint8_t* in, const void* desc, void* out, int N, int OH, int OW, float m0,
                                float m1, float m2, hipStream_t s) {
   dim3 grid((OH * OW + 255) / 256, N);
-  hipLaunchKernelGGL(drn::vgg_preprocess_kernel, grid, dim3(256), 0, s, in, (const drn::ImgDesc*)desc, (bf16_t*)out,
+  drn::launch(drn::vgg_preprocess_kernel, grid, dim3(256), 0, s, in, (const drn::ImgDesc*)desc, (bf16_t*)out,
                      OH, OW, m0, m1, m2);
   return (int)hipGetLastError();
 }
@@ -135,6 +135,6 @@ DRN_API int drn_vgg_preprocess(const uint8_t* in, const void* desc, void* out, i
 DRN_API int drn_synthetic_images(void* out, int64_t npix, uint32_t seed, hipStream_t s) {
   int64_t b = (npix + 255) / 256;
   if (b > 8192) b = 8192;
-  hipLaunchKernelGGL(drn::synthetic_images_kernel, dim3((int)b), dim3(256), 0, s, (bf16_t*)out, npix, seed);
+  drn::launch(drn::synthetic_images_kernel, dim3((int)b), dim3(256), 0, s, (bf16_t*)out, npix, seed);
   return (int)hipGetLastError();
 }

@@ -621,7 +621,7 @@ DRN_API int drn_bn_stats_blocks(int M, int C, int rows_per_block) { return (M + 
 DRN_API int drn_bn_stats(const void* x, float* part, int M, int C, int rows_per_block, int rep, hipStream_t s) {
   if (C % 8 || C / 8 > 256 || rep < 1) return (int)hipErrorInvalidValue;
   const int G = (M + rows_per_block - 1) / rows_per_block;
-  hipLaunchKernelGGL(drn::bn_stats_kernel, dim3(G), dim3(256), 256 * 17 * 4, s, (const bf16_t*)x, part, M, C,
+  drn::launch(drn::bn_stats_kernel, dim3(G), dim3(256), 256 * 17 * 4, s, (const bf16_t*)x, part, M, C,
                      rows_per_block, rep);
   return (int)hipGetLastError();
 }
@@ -629,7 +629,7 @@ DRN_API int drn_bn_stats(const void* x, float* part, int M, int C, int rows_per_
 DRN_API int drn_bn_finalize(float* part, int G, int C, float count, const float* gamma, const float* beta,
                             float eps, float momentum, float* run_mean, float* run_var, float* scale, float* shift,
                             float* mean, float* invstd, hipStream_t s) {
-  hipLaunchKernelGGL(drn::bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, G, C, count, gamma, beta,
+  drn::launch(drn::bn_finalize_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, G, C, count, gamma, beta,
                      eps, momentum, run_mean, run_var, scale, shift, mean, invstd);
   return (int)hipGetLastError();
 }
@@ -637,7 +637,7 @@ DRN_API int drn_bn_finalize(float* part, int G, int C, float count, const float*
 DRN_API int drn_bn_inference_params(int C, const float* gamma, const float* beta, const float* run_mean,
                                     const float* run_var, float eps, float* scale, float* shift, float* mean,
                                     float* invstd, hipStream_t s) {
-  hipLaunchKernelGGL(drn::bn_inference_params_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, beta,
+  drn::launch(drn::bn_inference_params_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, gamma, beta,
                      run_mean, run_var, eps, scale, shift, mean, invstd);
   return (int)hipGetLastError();
 }
@@ -646,7 +646,7 @@ DRN_API int drn_bn_apply(const void* x, void* y, const float* scale, const float
                          hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
   const int64_t nvec = M * (C / 8);
-  hipLaunchKernelGGL(drn::bn_apply_kernel, dim3(drn::grid_for(nvec)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y,
+  drn::launch(drn::bn_apply_kernel, dim3(drn::grid_for(nvec)), dim3(256), 0, s, (const bf16_t*)x, (bf16_t*)y,
                      scale, shift, nvec, C / 8, relu);
   return (int)hipGetLastError();
 }
@@ -657,7 +657,7 @@ DRN_API int drn_bn_apply_stats(const void* x, void* y, const float* acc, float c
                                hipStream_t s) {
   if (C % 8 || !pow2(C / 8) || C / 8 > 256) return (int)hipErrorInvalidValue;
   const int64_t nvec = M * (C / 8);
-  hipLaunchKernelGGL(drn::bn_apply_stats_kernel, dim3(drn::grid_for(nvec)), dim3(256), 0, s, (const bf16_t*)x,
+  drn::launch(drn::bn_apply_stats_kernel, dim3(drn::grid_for(nvec)), dim3(256), 0, s, (const bf16_t*)x,
                      (bf16_t*)y, acc, count, gamma, beta, eps, momentum, run_mean, run_var, scale, shift, mean, invstd,
                      nvec, C / 8, relu);
   return (int)hipGetLastError();
@@ -670,7 +670,7 @@ DRN_API int drn_bn_bwd_apply_stats(const void* dy, const float* dpool, int pool_
   if (C % 8 || !pow2(C / 8) || C / 8 > 256) return (int)hipErrorInvalidValue;
   const int64_t nvec = M * (C / 8);
   drn::DySrc src{(const bf16_t*)dy, dpool, pool_hw};
-  hipLaunchKernelGGL(drn::bn_bwd_apply_stats_kernel, dim3(drn::grid_for(nvec)), dim3(256), 0, s, src,
+  drn::launch(drn::bn_bwd_apply_stats_kernel, dim3(drn::grid_for(nvec)), dim3(256), 0, s, src,
                      (const bf16_t*)x, scale, shift, mean, invstd, acc, count, gamma, dgamma, dbeta,
                      (const bf16_t*)add, (bf16_t*)dx, nvec, C, relu);
   return (int)hipGetLastError();
@@ -682,14 +682,14 @@ DRN_API int drn_bn_bwd_reduce(const void* dy, const float* dpool, int pool_hw, c
   if (C % 8 || C / 8 > 256 || rep < 1) return (int)hipErrorInvalidValue;
   const int G = (M + rows_per_block - 1) / rows_per_block;
   drn::DySrc src{(const bf16_t*)dy, dpool, pool_hw};
-  hipLaunchKernelGGL(drn::bn_bwd_reduce_kernel, dim3(G), dim3(256), 256 * 17 * 4, s, src, (const bf16_t*)x, scale,
+  drn::launch(drn::bn_bwd_reduce_kernel, dim3(G), dim3(256), 256 * 17 * 4, s, src, (const bf16_t*)x, scale,
                      shift, mean, invstd, part, M, C, rows_per_block, relu, rep);
   return (int)hipGetLastError();
 }
 
 DRN_API int drn_bn_finalize_bwd(float* part, int G, int C, float count, const float* gamma,
                                 const float* invstd, float* dgamma, float* dbeta, float* coef, hipStream_t s) {
-  hipLaunchKernelGGL(drn::bn_finalize_bwd_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, G, C, count, gamma,
+  drn::launch(drn::bn_finalize_bwd_kernel, dim3((C + 63) / 64), dim3(256), 0, s, part, G, C, count, gamma,
                      invstd, dgamma, dbeta, coef);
   return (int)hipGetLastError();
 }
@@ -703,7 +703,7 @@ DRN_API int drn_bn_fin_fwd_launch(const DrnBnFin* f, hipStream_t s) {
   if (!fin_ok(f, f ? f->C : 0) || f->beta == nullptr || f->scale == nullptr || f->shift == nullptr ||
       f->mean == nullptr || f->invstd == nullptr)
     return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(drn::bn_fin_fwd_kernel, dim3((f->C + 255) / 256), dim3(256), 0, s, *f);
+  drn::launch(drn::bn_fin_fwd_kernel, dim3((f->C + 255) / 256), dim3(256), 0, s, *f);
   return (int)hipGetLastError();
 }
 
@@ -712,7 +712,7 @@ DRN_API int drn_bn_apply_fin(const void* x, void* y, const DrnBnFin* f, int64_t 
       (f->publish && (f->scale == nullptr || f->shift == nullptr || f->mean == nullptr || f->invstd == nullptr)))
     return (int)hipErrorInvalidValue;
   const int64_t nvec = M * (C / 8);
-  hipLaunchKernelGGL(drn::bn_apply_fin_kernel, dim3(drn::grid_for(nvec, 2)), dim3(256), 2 * C * sizeof(float), s,
+  drn::launch(drn::bn_apply_fin_kernel, dim3(drn::grid_for(nvec, 2)), dim3(256), 2 * C * sizeof(float), s,
                      (const bf16_t*)x, (bf16_t*)y, *f, nvec, C / 8, relu);
   return (int)hipGetLastError();
 }
@@ -729,7 +729,7 @@ DRN_API int drn_bn_bwd_apply_fin(const void* dy, const float* dpool, int pool_hw
   const dim3 grid(drn::grid_for(nvec, 4, 1024));  // 4 workgroups per CU (<= 128 VGPRs)
   const size_t lds = 3 * C * sizeof(float);
 #define DRN_BWD_FIN(ADD, POOL)                                                                                     \
-  hipLaunchKernelGGL((drn::bn_bwd_apply_fin_kernel<ADD, POOL>), grid, dim3(256), lds, s, src, (const bf16_t*)x, scale, \
+  drn::launch((drn::bn_bwd_apply_fin_kernel<ADD, POOL>), grid, dim3(256), lds, s, src, (const bf16_t*)x, scale, \
                      shift, *f, (const bf16_t*)add, (bf16_t*)dx, nvec, C, relu)
   if (pool_hw > 0) {
     if (add != nullptr) DRN_BWD_FIN(true, true);
@@ -755,7 +755,7 @@ DRN_API int drn_bn_bwd_apply(const void* dy, const float* dpool, int pool_hw, co
   drn::DySrc src{(const bf16_t*)dy, dpool, pool_hw};
   const dim3 grid(drn::grid_for(nvec, 4, 1024));  // 4 workgroups per CU (<= 128 VGPRs)
 #define DRN_BWD(ADD, POOL)                                                                                         \
-  hipLaunchKernelGGL((drn::bn_bwd_apply_kernel<ADD, POOL>), grid, dim3(256), 0, s, src, (const bf16_t*)x, scale, shift, \
+  drn::launch((drn::bn_bwd_apply_kernel<ADD, POOL>), grid, dim3(256), 0, s, src, (const bf16_t*)x, scale, shift, \
                      mean, invstd, coef, (const bf16_t*)add, (bf16_t*)dx, nvec, C, relu)
   if (pool_hw > 0) {
     if (add != nullptr) DRN_BWD(true, true);

@@ -903,7 +903,7 @@ static int launch_conv_nk_k(DrnConvFwdArgs* a, hipStream_t stream) {
     attr_set = true;
   }
   a->tiles_p = (M + BP - 1) / BP;
-  hipLaunchKernelGGL(kern, dim3(a->tiles_p), dim3(NW * 64), LDS, stream, *a);
+  drn::launch(kern, dim3(a->tiles_p), dim3(NW * 64), LDS, stream, *a);
   return (int)hipGetLastError();
 }
 
@@ -1023,7 +1023,7 @@ static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t 
                             160 * 1024);
         sk_attr_set = true;
       }
-      hipLaunchKernelGGL(skern, dim3(a->sk_blocks), dim3(NW * 64), LDS, stream, *a, zero);
+      drn::launch(skern, dim3(a->sk_blocks), dim3(NW * 64), LDS, stream, *a, zero);
       return (int)hipGetLastError();
     }
   }
@@ -1039,10 +1039,10 @@ static int launch_conv_glds_pf(DrnConvFwdArgs* a, const void* zero, hipStream_t 
     }
     DrnConvFwdArgs b = *a;
     b.in_fin.stats = nullptr;
-    hipLaunchKernelGGL(kern, dim3(tiles_p * tiles_c * ks), dim3(NW * 64), LDS, stream, b, zero);
+    drn::launch(kern, dim3(tiles_p * tiles_c * ks), dim3(NW * 64), LDS, stream, b, zero);
     return (int)hipGetLastError();
   }
-  hipLaunchKernelGGL(kern, dim3(tiles_p * tiles_c * ks), dim3(NW * 64), LDS, stream, *a, zero);
+  drn::launch(kern, dim3(tiles_p * tiles_c * ks), dim3(NW * 64), LDS, stream, *a, zero);
   return (int)hipGetLastError();
 }
 
@@ -1224,7 +1224,7 @@ static int launch_conv_fwd(DrnConvFwdArgs* a, hipStream_t stream) {
   const int tiles_p = (M + BP - 1) / BP;
   const int tiles_c = (a->K + BC - 1) / BC;
   a->tiles_p = tiles_p;
-  hipLaunchKernelGGL(kern, dim3(tiles_p * tiles_c), dim3(256), LDS, stream, *a);
+  drn::launch(kern, dim3(tiles_p * tiles_c), dim3(256), LDS, stream, *a);
   return (int)hipGetLastError();
 }
 

@@ -280,7 +280,7 @@ static int launch_wgrad(DrnConvWgradArgs* a, hipStream_t s) {
   const int Ktot = a->R * a->S * a->C;
   const int nkt = (Ktot + BKK - 1) / BKK;
   const int nct = (a->K + BCO - 1) / BCO;
-  hipLaunchKernelGGL(kern, dim3(nkt * nct, a->splits), dim3(256), LDS, s, *a);
+  drn::launch(kern, dim3(nkt * nct, a->splits), dim3(256), LDS, s, *a);
   return (int)hipGetLastError();
 }
 
@@ -723,7 +723,7 @@ static int launch_wgrad_glds_p(DrnConvWgradArgs* a, const void* zero, hipStream_
   const int Ktot = a->R * a->S * a->C;
   const int nkt = (Ktot + BKK - 1) / BKK;
   const int nct = (a->K + BCO - 1) / BCO;
-  hipLaunchKernelGGL(kern, dim3(nkt * nct, a->splits), dim3(256), LDS, s, *a, zero);
+  drn::launch(kern, dim3(nkt * nct, a->splits), dim3(256), LDS, s, *a, zero);
   return (int)hipGetLastError();
 }
 
@@ -894,13 +894,13 @@ DRN_API int drn_splitk_reduce(const float* ws, float* out, int64_t n, int splits
   const int cols = (n4 >= 512 * 64 || splits <= 8) ? 64 : (n4 >= 512 * 16 || splits <= 32) ? 16 : 4;
   const int blocks = n4 > 0 ? (n4 + cols - 1) / cols : 1;
   if (cols == 64)
-    hipLaunchKernelGGL(drn::splitk_reduce_kernel<64>, dim3(blocks), dim3(256), 0, s, ws, out, n4, splits, (size_t)n4,
+    drn::launch(drn::splitk_reduce_kernel<64>, dim3(blocks), dim3(256), 0, s, ws, out, n4, splits, (size_t)n4,
                        scale, accumulate);
   else if (cols == 16)
-    hipLaunchKernelGGL(drn::splitk_reduce_kernel<16>, dim3(blocks), dim3(256), 0, s, ws, out, n4, splits, (size_t)n4,
+    drn::launch(drn::splitk_reduce_kernel<16>, dim3(blocks), dim3(256), 0, s, ws, out, n4, splits, (size_t)n4,
                        scale, accumulate);
   else
-    hipLaunchKernelGGL(drn::splitk_reduce_kernel<4>, dim3(blocks), dim3(256), 0, s, ws, out, n4, splits, (size_t)n4,
+    drn::launch(drn::splitk_reduce_kernel<4>, dim3(blocks), dim3(256), 0, s, ws, out, n4, splits, (size_t)n4,
                        scale, accumulate);
   return (int)hipGetLastError();
 }

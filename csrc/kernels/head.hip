@@ -248,7 +248,7 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ i
 DRN_API int drn_bnrelu_pool(const void* x, const float* scale, const float* shift, float* pooled, int N, int HW,
                             int C, int relu, hipStream_t s) {
   if (C % 8) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(drn::bnrelu_pool_kernel, dim3(N), dim3(256), 0, s, (const bf16_t*)x, scale, shift, pooled, HW, C,
+  drn::launch(drn::bnrelu_pool_kernel, dim3(N), dim3(256), 0, s, (const bf16_t*)x, scale, shift, pooled, HW, C,
                      relu);
   return (int)hipGetLastError();
 }
@@ -259,23 +259,23 @@ DRN_API int drn_sgemm(int ta, int tb, int M, int N, int K, float alpha, const fl
                       hipStream_t s) {
   if (splits < 1 || (splits > 1 && ws == nullptr)) return (int)hipErrorInvalidValue;
   dim3 grid((N + 63) / 64, (M + 63) / 64, splits);
-  hipLaunchKernelGGL(drn::sgemm_kernel, grid, dim3(256), 0, s, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta,
+  drn::launch(drn::sgemm_kernel, grid, dim3(256), 0, s, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta,
                      splits > 1 ? ws : C, ldc, bias);
   if (splits > 1)
-    hipLaunchKernelGGL(drn::sgemm_finish_kernel, dim3((M * N + 255) / 256), dim3(256), 0, s, ws, splits, M, N, ldc,
+    drn::launch(drn::sgemm_finish_kernel, dim3((M * N + 255) / 256), dim3(256), 0, s, ws, splits, M, N, ldc,
                        alpha, beta, C, bias);
   return (int)hipGetLastError();
 }
 
 DRN_API int drn_softmax_xent(const float* logits, const int* labels, int N, int ncls, float grad_scale,
                              float* dlogits, float* loss, float* probs, int* correct, hipStream_t s) {
-  hipLaunchKernelGGL(drn::softmax_xent_kernel, dim3(N), dim3(256), 0, s, logits, labels, ncls, grad_scale, dlogits,
+  drn::launch(drn::softmax_xent_kernel, dim3(N), dim3(256), 0, s, logits, labels, ncls, grad_scale, dlogits,
                      loss, probs, correct);
   return (int)hipGetLastError();
 }
 
 DRN_API int drn_colsum(const float* in, int rows, int cols, float* out, float scale, int accumulate, hipStream_t s) {
-  hipLaunchKernelGGL(drn::colsum_kernel, dim3((cols + 31) / 32), dim3(256), 0, s, in, rows, cols, out, scale,
+  drn::launch(drn::colsum_kernel, dim3((cols + 31) / 32), dim3(256), 0, s, in, rows, cols, out, scale,
                      accumulate);
   return (int)hipGetLastError();
 }

@@ -1,0 +1,152 @@
+// plan.hip — native step launcher: a recorded training step replayed from C++.
+//
+// The eager step of the executor (runtime/executor.py) is a fixed sequence of ~340 kernel launches
+// on two streams (the high-priority critical-path stream and the weight-gradient side stream) plus
+// the cross-stream event records / waits that order them. Issued from Python every launch costs
+// ~19 us of host time (ctypes marshalling of the argument block, geometry keys, stream objects):
+// 6.4 ms per ResNet-50 step, 3-5 ms per CIFAR step -- the host, not the GPU, bounds the CIFAR
+// steps and any future faster ImageNet step. A HIP graph removes that cost but replays every
+// branch from one normal-priority queue (ResNet-50: 10.4 vs 9.6 ms eager).
+//
+// A Plan keeps the eager structure and drops the Python: while the calling thread records
+// (drn_plan_record_begin .. _end), every drn::launch of the library appends {kernel, grid, block,
+// LDS, stream, by-value argument copy} instead of launching (drn_common.h), and the runtime adds
+// event-record / stream-wait entries (drn_plan_event_record / drn_plan_stream_wait) where the
+// Python step would have called torch's stream API. drn_plan_replay(begin, end) then re-issues
+// entries [begin, end) with hipLaunchKernel / hipEventRecord / hipStreamWaitEvent: the same
+// kernels, arguments, streams and priorities as the eager step, one host call per segment (the
+// data-parallel step is cut at the points where a bucket collective is issued from Python).
+// The equivalent of the reference's per-step `mon_sess.run(train_op)` executor call
+// (resnet_cifar_main.py:320-321).
+#include "drn_common.h"
+
+#include <memory>
+#include <vector>
+
+namespace drn {
+
+thread_local Plan* g_plan_rec = nullptr;
+
+struct PlanEntry {
+  enum Kind : int { LAUNCH = 0, RECORD = 1, WAIT = 2 };
+  int kind = LAUNCH;
+  const void* fn = nullptr;
+  dim3 grid, block;
+  size_t shm = 0;
+  hipStream_t stream = nullptr;
+  void* blob = nullptr;
+  void** argv = nullptr;
+  void (*del)(void*) = nullptr;
+  int ev = -1;
+};
+
+struct Plan {
+  std::vector<PlanEntry> e;
+  std::vector<hipEvent_t> events;
+  int launches = 0;
+  ~Plan() {
+    for (auto& x : e) {
+      if (x.del != nullptr) x.del(x.blob);
+      delete[] x.argv;
+    }
+    for (auto ev : events) hipEventDestroy(ev);
+  }
+};
+
+void plan_add_launch(Plan* p, const void* fn, dim3 grid, dim3 block, size_t shm, hipStream_t s, void* blob,
+                     void** argv, void (*del)(void*)) {
+  PlanEntry x;
+  x.kind = PlanEntry::LAUNCH;
+  x.fn = fn;
+  x.grid = grid;
+  x.block = block;
+  x.shm = shm;
+  x.stream = s;
+  x.blob = blob;
+  x.argv = argv;
+  x.del = del;
+  p->e.push_back(x);
+  ++p->launches;
+}
+
+}  // namespace drn
+
+using drn::Plan;
+using drn::PlanEntry;
+
+DRN_API void* drn_plan_create() { return new Plan(); }
+
+DRN_API void drn_plan_destroy(void* p) { delete static_cast<Plan*>(p); }
+
+// Start / stop recording the calling thread's launches into p (one plan per thread at a time).
+DRN_API int drn_plan_record_begin(void* p) {
+  if (p == nullptr || drn::g_plan_rec != nullptr) return (int)hipErrorInvalidValue;
+  drn::g_plan_rec = static_cast<Plan*>(p);
+  return 0;
+}
+
+DRN_API int drn_plan_record_end() {
+  if (drn::g_plan_rec == nullptr) return (int)hipErrorInvalidValue;
+  drn::g_plan_rec = nullptr;
+  return 0;
+}
+
+// A new (timing-disabled) event of the plan; returns its index.
+DRN_API int drn_plan_new_event(void* pv) {
+  Plan* p = static_cast<Plan*>(pv);
+  hipEvent_t ev;
+  const hipError_t rc = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (rc != hipSuccess) return -(int)rc;
+  p->events.push_back(ev);
+  return (int)p->events.size() - 1;
+}
+
+DRN_API int drn_plan_event_record(void* pv, int ev, hipStream_t s) {
+  Plan* p = static_cast<Plan*>(pv);
+  if (ev < 0 || ev >= (int)p->events.size()) return (int)hipErrorInvalidValue;
+  PlanEntry x;
+  x.kind = PlanEntry::RECORD;
+  x.ev = ev;
+  x.stream = s;
+  p->e.push_back(x);
+  return 0;
+}
+
+DRN_API int drn_plan_stream_wait(void* pv, hipStream_t s, int ev) {
+  Plan* p = static_cast<Plan*>(pv);
+  if (ev < 0 || ev >= (int)p->events.size()) return (int)hipErrorInvalidValue;
+  PlanEntry x;
+  x.kind = PlanEntry::WAIT;
+  x.ev = ev;
+  x.stream = s;
+  p->e.push_back(x);
+  return 0;
+}
+
+// Entries recorded so far (segment boundaries are entry positions).
+DRN_API int drn_plan_size(void* pv) { return (int)static_cast<Plan*>(pv)->e.size(); }
+
+DRN_API int drn_plan_launches(void* pv) { return static_cast<Plan*>(pv)->launches; }
+
+// Re-issue entries [begin, end) in order; stops at and returns the first HIP error.
+DRN_API int drn_plan_replay(void* pv, int begin, int end) {
+  Plan* p = static_cast<Plan*>(pv);
+  if (begin < 0 || end > (int)p->e.size() || begin > end) return (int)hipErrorInvalidValue;
+  for (int i = begin; i < end; ++i) {
+    const PlanEntry& x = p->e[i];
+    hipError_t rc;
+    switch (x.kind) {
+      case PlanEntry::LAUNCH:
+        rc = hipLaunchKernel(x.fn, x.grid, x.block, x.argv, x.shm, x.stream);
+        break;
+      case PlanEntry::RECORD:
+        rc = hipEventRecord(p->events[x.ev], x.stream);
+        break;
+      default:
+        rc = hipStreamWaitEvent(x.stream, p->events[x.ev], 0);
+        break;
+    }
+    if (rc != hipSuccess) return (int)rc;
+  }
+  return 0;
+}

@@ -254,7 +254,7 @@ DRN_API int drn_maxpool_fwd(const void* x, void* y, uint8_t* arg, int N, int H, 
   const int rows = N * P;
   const int rpb = rows >= 4096 ? 4 : 1;  // ~1.8K blocks at the ImageNet stem (128 x 56 rows)
   auto kern = k == 3 ? drn::maxpool_fwd_kernel<3> : drn::maxpool_fwd_kernel<0>;
-  hipLaunchKernelGGL(kern, dim3((rows + rpb - 1) / rpb), dim3(256), part ? 256 * 17 * 4 : 0, s, (const bf16_t*)x,
+  drn::launch(kern, dim3((rows + rpb - 1) / rpb), dim3(256), part ? 256 * 17 * 4 : 0, s, (const bf16_t*)x,
                      (bf16_t*)y, arg, N, H, W, C, P, Q, k, stride, pad_h, pad_w, rpb, part, rep);
   return (int)hipGetLastError();
 }
@@ -265,12 +265,12 @@ DRN_API int drn_maxpool_bwd(const void* dy, const uint8_t* arg, void* dx, int N,
   if (stride == 2 && k <= 4) {
     const int64_t total = (int64_t)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
     auto kern = k <= 3 ? drn::maxpool_bwd_s2_flat_kernel<2> : drn::maxpool_bwd_s2_flat_kernel<3>;
-    hipLaunchKernelGGL(kern, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, (const bf16_t*)dy, arg,
+    drn::launch(kern, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, (const bf16_t*)dy, arg,
                        (bf16_t*)dx, N, H, W, C, P, Q, k, pad_h, pad_w);
     return (int)hipGetLastError();
   }
   const int64_t total = (int64_t)N * H * W * (C / 8);
-  hipLaunchKernelGGL(drn::maxpool_bwd_kernel, dim3(drn::grid_for(total)), dim3(256), 0, s, (const bf16_t*)dy, arg,
+  drn::launch(drn::maxpool_bwd_kernel, dim3(drn::grid_for(total)), dim3(256), 0, s, (const bf16_t*)dy, arg,
                      (bf16_t*)dx, N, H, W, C, P, Q, k, stride, pad_h, pad_w);
   return (int)hipGetLastError();
 }

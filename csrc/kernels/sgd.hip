@@ -167,30 +167,30 @@ DRN_API int drn_sgd_momentum(float* w, float* m, const void* g, int g_bf16, void
                              hipStream_t s) {
   if (n % 4) return (int)hipErrorInvalidValue;
   if (g_bf16)
-    hipLaunchKernelGGL(drn::sgd_momentum_kernel<bf16_t>, dim3(drn::grid_for(n / 4)), dim3(256), 0, s, w, m,
+    drn::launch(drn::sgd_momentum_kernel<bf16_t>, dim3(drn::grid_for(n / 4)), dim3(256), 0, s, w, m,
                        (const bf16_t*)g, (bf16_t*)w_bf16, n / 4, lr_ptr, momentum, wd, grad_scale, skip);
   else
-    hipLaunchKernelGGL(drn::sgd_momentum_kernel<float>, dim3(drn::grid_for(n / 4)), dim3(256), 0, s, w, m,
+    drn::launch(drn::sgd_momentum_kernel<float>, dim3(drn::grid_for(n / 4)), dim3(256), 0, s, w, m,
                        (const float*)g, (bf16_t*)w_bf16, n / 4, lr_ptr, momentum, wd, grad_scale, skip);
   return (int)hipGetLastError();
 }
 
 DRN_API int drn_cast_bf16(const float* x, void* y, int64_t n, hipStream_t s) {
   if (n % 4) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(drn::cast_bf16_kernel, dim3(drn::grid_for(n / 4)), dim3(256), 0, s, x, (bf16_t*)y, n / 4);
+  drn::launch(drn::cast_bf16_kernel, dim3(drn::grid_for(n / 4)), dim3(256), 0, s, x, (bf16_t*)y, n / 4);
   return (int)hipGetLastError();
 }
 
 // total = number of tiles (last begin + its count); every descriptor has K % 8 == C % 8 == 0.
 DRN_API int drn_weight_tflip(const void* w, void* wt, const void* table, int ntab, int64_t total, hipStream_t s) {
   if (ntab < 1 || total < 1 || total > 0x7fffffff) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(drn::weight_tflip_kernel, dim3((unsigned)total), dim3(256), 0, s, (const bf16_t*)w,
+  drn::launch(drn::weight_tflip_kernel, dim3((unsigned)total), dim3(256), 0, s, (const bf16_t*)w,
                      (bf16_t*)wt, (const drn::TDesc*)table, ntab);
   return (int)hipGetLastError();
 }
 
 DRN_API int drn_fill_f32(float* x, int64_t n, float v, hipStream_t s) {
-  hipLaunchKernelGGL(drn::fill_f32_kernel, dim3(drn::grid_for(n)), dim3(256), 0, s, x, n, v);
+  drn::launch(drn::fill_f32_kernel, dim3(drn::grid_for(n)), dim3(256), 0, s, x, n, v);
   return (int)hipGetLastError();
 }
 

@@ -71,7 +71,7 @@ DRN_API int drn_stem_pack_input(const void* x, void* xp, int rows, int W, hipStr
   const int64_t np = (int64_t)rows * (W / 2);
   int64_t blocks = (np + 255) / 256;
   if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(drn::stem_pack_input_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const bf16_t*)x,
+  drn::launch(drn::stem_pack_input_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const bf16_t*)x,
                      (bf16_t*)xp, rows, W, np);
   return (int)hipGetLastError();
 }
@@ -80,7 +80,7 @@ DRN_API int drn_stem_pack_weights(const void* w, void* wp, int K, int R, int S, 
                                   hipStream_t s) {
   if (S8 < S || C4 > C) return (int)hipErrorInvalidValue;
   const int n = K * R * S8 * C4;
-  hipLaunchKernelGGL(drn::stem_pack_weights_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const bf16_t*)w,
+  drn::launch(drn::stem_pack_weights_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const bf16_t*)w,
                      (bf16_t*)wp, K, R, S, C, S8, C4);
   return (int)hipGetLastError();
 }
@@ -89,7 +89,7 @@ DRN_API int drn_stem_unpack_grad(const float* dwp, float* dw, int K, int R, int 
                                  hipStream_t s) {
   if (S8 < S || C4 > C) return (int)hipErrorInvalidValue;
   const int n = K * R * S * C;
-  hipLaunchKernelGGL(drn::stem_unpack_grad_kernel, dim3((n + 255) / 256), dim3(256), 0, s, dwp, dw, K, R, S, C, S8,
+  drn::launch(drn::stem_unpack_grad_kernel, dim3((n + 255) / 256), dim3(256), 0, s, dwp, dw, K, R, S, C, S8,
                      C4);
   return (int)hipGetLastError();
 }

@@ -139,6 +139,17 @@ _SIGS = {
     "drn_bn_apply_fin": ([c_p, c_p, c_p, c_i64, c_int, c_int, c_p], c_int),
     "drn_bn_bwd_apply_fin": ([c_p, c_p, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_int, c_int, c_p], c_int),
     "drn_synthetic_images": ([c_p, c_i64, ctypes.c_uint32, c_p], c_int),
+    # native step plans (csrc/kernels/plan.hip, runtime/plan.py)
+    "drn_plan_create": ([], c_p),
+    "drn_plan_destroy": ([c_p], None),
+    "drn_plan_record_begin": ([c_p], c_int),
+    "drn_plan_record_end": ([], c_int),
+    "drn_plan_new_event": ([c_p], c_int),
+    "drn_plan_event_record": ([c_p, c_int, c_p], c_int),
+    "drn_plan_stream_wait": ([c_p, c_p, c_int], c_int),
+    "drn_plan_size": ([c_p], c_int),
+    "drn_plan_launches": ([c_p], c_int),
+    "drn_plan_replay": ([c_p, c_int, c_int], c_int),
 }
 
 

@@ -255,6 +255,7 @@ class HipBackend(_Common):
         self._fin_bufs: dict = {}
         self.conv_cands: dict = {}   # geometry key -> tuner finalists, fastest first
         self._insitu = None          # list of (key, cfg, ev0, ev1) while Executor.insitu_tune runs
+        self.recording = False       # a native step plan is being recorded (runtime/plan.py)
 
     def _timed(self, launch, n: int) -> float:
         """Mean ms of n back-to-back launches of launch() on the current stream."""
@@ -395,7 +396,9 @@ class HipBackend(_Common):
     def launch_conv(self, a):
         if a.cfg == -1 and self.autotune and self.forced_cfg is None:
             key = self.conv_key(a)
-            if key not in self.conv_cfg and not torch.cuda.is_current_stream_capturing():
+            if key not in self.conv_cfg and (self.recording or torch.cuda.is_current_stream_capturing()):
+                raise RuntimeError(f"untuned convolution {key} while recording a step (tune it eagerly first)")
+            if key not in self.conv_cfg:
                 hit = self.tune_db().get_conv(key)
                 if hit is not None and self._conv_hit_ok(a, hit):
                     self.db_hits += 1
@@ -640,6 +643,8 @@ class HipBackend(_Common):
             self._wgrad_full(a, self.forced_wgrad_ns, out, st)
             return
         key = self.wgrad_key(a)
+        if key not in self.wgrad_ns and self.autotune and self.recording:
+            raise RuntimeError(f"untuned weight gradient {key} while recording a step (tune it eagerly first)")
         if key not in self.wgrad_ns and self.autotune and not torch.cuda.is_current_stream_capturing():
             hit = self.tune_db().get_wgrad(key)
             cands = [int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6,7,8").split(",")]

@@ -158,6 +158,13 @@ class Executor:
         # the main stream has waited for the side stream up to _synced
         self._pending = {}
         self._marks = {}
+        # data parallelism: the stream bucket collectives are issued from (_report)
+        self._report_stream = None
+        self._reported = False
+        # cross-stream ordering goes through a scheduler: torch's stream API, or -- while a native
+        # step plan is recorded (runtime/plan.py) -- plan event entries replayed from C++
+        from .plan import TorchSched
+        self.sched = TorchSched()
         self._wseq = 0
         self._synced = 0
         # a claim that needs a wait waits on the side-stream mark up to claim_span weight
@@ -652,7 +659,7 @@ class Executor:
         # dense layer: its weight / bias gradients only feed the optimizer, so with the side
         # stream they run there, off the data-gradient chain
         if self.side is not None:
-            self.side.wait_stream(torch.cuda.current_stream(self.device))
+            self.sched.wait_stream(self.side, torch.cuda.current_stream(self.device))
             with torch.cuda.stream(self.side):
                 be.sgemm(1, 0, ncls, C, N, 1.0, self.dlogits, ncls, self.pooled, C, 0.0, self.dense_dw, C)
                 be.colsum(self.dlogits, self.dense_db)
@@ -675,7 +682,7 @@ class Executor:
             # (a capture starts after its eager warm-up has synchronized: the event is complete,
             # and a graph may not wait on an event recorded outside it)
             if not (self.is_hip and torch.cuda.is_current_stream_capturing()):
-                torch.cuda.current_stream(self.device).wait_event(self._tflip_ev)
+                self.sched.wait(torch.cuda.current_stream(self.device), self._tflip_ev, key="tflip")
             self._tflip_ev = None
         for bp in reversed(self.blocks):
             cur = self._block_bwd(bp, bufs, cur)
@@ -698,8 +705,7 @@ class Executor:
             # every weight gradient but the stem's is issued on the side stream: the optimizer
             # may update those while the stem's weight gradient (the last, ~0.2 ms on ImageNet)
             # still runs -- see apply_gradients
-            self._tail_ev = torch.cuda.Event()
-            self._tail_ev.record(self.side)
+            self._tail_ev = self.sched.record(self.side)
         if self.stem_pack:
             if getattr(be, "wgrad_atomic_used", False):
                 be.zero_(self.stem_dw4)
@@ -708,18 +714,23 @@ class Executor:
         else:
             self._wgrad(self.images, d_stem, st.dw, st.geom)
         if self._tail_ev is not None:
-            self._stem_ev = torch.cuda.Event()
-            self._stem_ev.record(self.side)
+            self._stem_ev = self.sched.record(self.side)
         self._report(0)
         if self._tail_ev is None:
             self._join()
 
     def _report(self, lo: int):
         """grad_ready(lo): every gradient at flat offsets >= lo is issued. With the weight-gradient
-        side stream the report is made FROM that stream after it has caught up with the main
-        stream, so the bucket collectives it launches are ordered after both streams' producers
-        while the main stream's data-gradient chain never waits for the side stream."""
+        side stream, a report that launches a bucket collective is issued from a dedicated report
+        stream that waits on two per-bucket readiness events -- the main stream's (the BN-backward
+        applies that published the bucket's dgamma / dbeta) and the side stream's (its weight
+        gradients) -- so the collective is ordered after exactly its producers while neither
+        compute stream waits for the other (round 4 made the SIDE stream catch up with the main
+        stream at every launching report, stalling the next blocks' weight gradients)."""
         if self.grad_ready is None:
+            return
+        if self.sched.recording:                         # a native plan is cut here: the report
+            self.sched.cut(("report", lo))               # runs from Python at each replay
             return
         if self.side is None:
             self.grad_ready(lo)
@@ -728,9 +739,15 @@ class Executor:
         if owner is not None and hasattr(owner, "launches_at") and not owner.launches_at(lo):
             self.grad_ready(lo)                          # (advances the frontier, launches nothing)
             return
-        self.side.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(self.side):
+        main = torch.cuda.current_stream(self.device)
+        if self._report_stream is None:
+            self._report_stream = torch.cuda.Stream(self.device)
+        rs = self._report_stream
+        rs.wait_stream(main)                             # readiness event of the main-stream producers
+        rs.wait_stream(self.side)                        # ... and of the weight gradients
+        with torch.cuda.stream(rs):
             self.grad_ready(lo)
+        self._reported = True
 
     # -- weight gradients on the side stream ---------------------------------------------------------
     def _wgrad(self, x, dy, dw, geom, in_bn=None, dy_buf=None, post=None):
@@ -742,16 +759,14 @@ class Executor:
                 post()
             return
         main = torch.cuda.current_stream(self.device)
-        self.side.wait_stream(main)                      # x and dy are complete
+        self.sched.wait_stream(self.side, main)          # x and dy are complete
         with torch.cuda.stream(self.side):
             self.be.conv_wgrad(x, dy, dw, geom, in_bn=in_bn, ws=self.wgrad_ws)
             if post is not None:
                 post()
         if dy_buf is not None:                           # the main stream must not overwrite dy early
             self._wseq += 1
-            ev = torch.cuda.Event()
-            ev.record(self.side)
-            self._marks[self._wseq] = ev
+            self._marks[self._wseq] = self.sched.record(self.side)
             self._pending[id(dy_buf)] = self._wseq
 
     def _claim(self, buf):
@@ -771,21 +786,24 @@ class Executor:
             del self._marks[k]
         # an event that has already completed needs no cross-queue barrier packet; inside a
         # capture the dependency must be recorded as a graph edge regardless
-        if self.claim_query and not torch.cuda.is_current_stream_capturing() and ev.query():
+        if self.claim_query and not torch.cuda.is_current_stream_capturing() and self.sched.done(ev):
             return
-        torch.cuda.current_stream(self.device).wait_event(ev)
+        self.sched.wait(torch.cuda.current_stream(self.device), ev)
 
     def _join(self, ev=None):
         if self.side is None:
             return
         main = torch.cuda.current_stream(self.device)
+        if self._reported:                               # (a capture must rejoin every forked stream)
+            main.wait_stream(self._report_stream)
+            self._reported = False
         if ev is None:
-            main.wait_stream(self.side)
+            self.sched.wait_stream(main, self.side)
             self._pending.clear()
             self._marks.clear()
             self._synced = self._wseq
         else:
-            main.wait_event(ev)
+            self.sched.wait(main, ev)
 
     def _dgrad(self, op: ConvOp, dy, dx, accumulate: bool, bn: Optional[BNState] = None, bn_x=None):
         """Data gradient of `op` into dx (+= when accumulate). With bn set (requires a launch set
@@ -873,7 +891,7 @@ class Executor:
             # parameters [stem_hi, end) while the stem's weight gradient finishes on the side
             # stream (the stem has no data-gradient weights, so the refresh goes first too)
             hi, ev = self._stem_hi, self._tail_ev
-            torch.cuda.current_stream(self.device).wait_event(ev)
+            self.sched.wait(torch.cuda.current_stream(self.device), ev)
             wb = P.wbf16[hi:] if P.wbf16 is not None else None
             self.be.sgd_momentum(P.master[hi:], P.momentum[hi:], g[hi:], wb, self.lr_t, self.mom, self.wd,
                                  grad_scale, skip)
@@ -908,11 +926,10 @@ class Executor:
             src = P.wbf16 if P.wbf16 is not None else P.master
             table = self.wt_table if self.is_hip else self.wt_table.cpu()
             if self.side is not None and self.tflip_side and not torch.cuda.is_current_stream_capturing():
-                self.side.wait_stream(torch.cuda.current_stream(self.device))  # the updated weights
+                self.sched.wait_stream(self.side, torch.cuda.current_stream(self.device))  # the updated weights
                 with torch.cuda.stream(self.side):
                     self.be.weight_tflip(src, self.wt_flat, table, self.wt_n, self.wt_total)
-                self._tflip_ev = torch.cuda.Event()
-                self._tflip_ev.record(self.side)
+                self._tflip_ev = self.sched.record(self.side, key="tflip")
             else:
                 self.be.weight_tflip(src, self.wt_flat, table, self.wt_n, self.wt_total)
         if stem:

@@ -74,8 +74,8 @@ def evaluate(FLAGS, eval_batch_size: int = 100, max_evals: int = -1):
                         if not feeder.next():
                             break
                         ex.forward(train=False)
-                        v = int(getattr(feeder, "valid", ex.N))
-                        feeder.prefetch()   # host load of the next batch while this one runs  # wrapped padding of a final partial batch
+                        v = int(getattr(feeder, "valid", ex.N))  # wrapped padding of a final partial batch
+                        feeder.prefetch()   # host load of the next batch while this one runs
                         total_loss += float(ex.loss_vec[:v].double().sum())
                         correct += int(ex.correct[:v].sum())
                         total += v

@@ -65,6 +65,7 @@ class _StagedFeeder:
         self.copy_stream = torch.cuda.Stream(device=ex.device) if self.gpu else None
         self._pending = None
         self._consumed = None          # event after the preprocess of the batch last handed out
+        self._main = None              # the stream that consumes the batches (set by next())
         self._need_prefetch = False
         self._pending_state, self._pending_valid = self.loader.state(), ex.N
         self._state, self.valid = self.loader.state(), ex.N
@@ -110,8 +111,9 @@ class _StagedFeeder:
         self._wait()
         self._consume()
         if self.gpu:
+            self._main = torch.cuda.current_stream(self.ex.device)
             self._consumed = torch.cuda.Event()
-            self._consumed.record(torch.cuda.current_stream(self.ex.device))
+            self._consumed.record(self._main)
         self._state, self.valid = self._pending_state, self._pending_valid
         self._need_prefetch = True
         return True
@@ -173,10 +175,19 @@ class ImagenetFeeder(_StagedFeeder):
             self.d_lab.copy_(_as_tensor(labels))
             return
         if n > self.d_buf.numel():
-            # stream-ordered reallocation: the old buffer is released only after the main
-            # stream's last reader of it (the previous preprocess) is done
-            torch.cuda.current_stream(self.ex.device).synchronize()
+            # reallocation (prefetch may run on a worker thread, whose current stream is NOT the
+            # consuming one): the old buffer is released only after the last preprocess that read
+            # it -- the event next() recorded on the consuming stream -- and the new one is
+            # marked in use by both streams that touch it, so the caching allocator never hands
+            # its memory out early
+            if self._consumed is not None:
+                self._consumed.synchronize()
+            else:
+                torch.cuda.synchronize(self.ex.device)
             self.d_buf = torch.empty(int(n * 1.25), dtype=torch.uint8, device=self.ex.device)
+            self.d_buf.record_stream(self.copy_stream)
+            if self._main is not None:
+                self.d_buf.record_stream(self._main)
         self._stage([(self.d_buf[:n], packed), (self.d_desc, desc_bytes), (self.d_lab, labels)])
 
     def _consume(self):

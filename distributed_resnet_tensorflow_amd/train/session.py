@@ -43,6 +43,21 @@ def make_backend(device: str, precision: str = "bf16"):
     return RefBackend("cpu")
 
 
+def agree_ms(values, group=None):
+    """The slowest rank's timings (element-wise MAX over the process group): every rank takes a
+    timing-based step-mode decision from the same numbers, so no two ranks end up in different
+    step modes (bench.py does the same for its graph / eager choice). Identity without an
+    initialised multi-rank group."""
+    import torch.distributed as dist
+    vals = [float(v) for v in values]
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) <= 1:
+        return vals
+    dev = "cpu" if dist.get_backend(group) == "gloo" else torch.device("cuda", torch.cuda.current_device())
+    t = torch.tensor(vals, dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return t.tolist()
+
+
 class _LazyGraph:
     """Placeholder graph: its first replay() captures the step (the StepGraph warm-up is that
     real step), later replays run the captured graph."""
@@ -125,7 +140,13 @@ class TrainingSession:
         self._side_trial = (self.use_graph and (self.engine is None or self.engine.p2p is not None)
                             and self.ex.side is not None and os.environ.get("DRN_SIDE_TRIAL", "1") == "1")
         self.side_choice: Optional[dict] = None
+        # graphs are captured and replayed from a NORMAL-priority stream (replay from the high-
+        # priority eager stream measured far slower: 19.4 vs 11.2 ms, parallel/engine.py), so when
+        # the eager step moves to the high-priority stream below, the segmented-graph candidate of
+        # the trial keeps this one
+        self._graph_stream = None
         if not self.use_graph and self.device.type == "cuda" and self.be.name == "hip":
+            self._graph_stream = torch.cuda.current_stream(self.device)
             # eager step (data parallel or not): the critical path on its own high-priority HW
             # queue, ahead of the weight-gradient side stream (ResNet-50 bs128 on one GPU: 9.93 vs
             # 10.17 ms per step, profiles/r3_side_stream_ab.txt)
@@ -175,6 +196,28 @@ class TrainingSession:
         return path
 
     # -- stepping ----------------------------------------------------------------------------------
+    def _on_graph_stream(self, fn):
+        """fn() on the normal-priority graph stream, ordered after and before the eager stream's
+        work (identity when the step never left that stream)."""
+        gs = self._graph_stream
+        if gs is None:
+            return fn()
+        cur = torch.cuda.current_stream(self.device)
+        gs.wait_stream(cur)
+        with torch.cuda.stream(gs):
+            r = fn()
+        cur.wait_stream(gs)
+        return r
+
+    def will_capture(self) -> bool:
+        """Whether the next step() captures a HIP graph (no other thread may then touch the GPU
+        in ways a global-mode capture forbids: the feeder's prefetch waits, TrainingSession.run)."""
+        if self.ex.check_nan:
+            return False
+        if self.use_graph and (self._graph is None or (isinstance(self._graph, _LazyGraph) and self._graph.g is None)):
+            return True
+        return self._trial is not None and self._trial[0] == "graph" and self._graph is None
+
     def _step_body(self):
         ex = self.ex
         with phase("fwd"):
@@ -200,7 +243,8 @@ class TrainingSession:
         if self.use_graph and not self.ex.check_nan:  # the debug checks synchronize: no capture
             if self._graph is None:  # warm-up = this real step
                 if self.engine is not None and self.engine.p2p is None:
-                    self._graph = SegmentedStepGraph(self.ex, self.engine, 1.0 / self.world, warmup=1)
+                    self._graph = self._on_graph_stream(
+                        lambda: SegmentedStepGraph(self.ex, self.engine, 1.0 / self.world, warmup=1))
                 else:
                     self._graph = StepGraph(self._step_body, warmup=1)
                     if self._side_trial:
@@ -213,7 +257,7 @@ class TrainingSession:
                 if hooks:
                     self.engine.replay_begin()
                 with phase("step (graph replay)"):
-                    self._graph.replay()
+                    self._on_graph_stream(self._graph.replay)
                 if hooks:
                     self.engine.replay_end()
                 if self._strial is not None:
@@ -251,17 +295,20 @@ class TrainingSession:
                 return
         else:
             if self._graph is None:
-                self._graph = SegmentedStepGraph(self.ex, self.engine, 1.0 / self.world, warmup=1)
+                self._graph = self._on_graph_stream(
+                    lambda: SegmentedStepGraph(self.ex, self.engine, 1.0 / self.world, warmup=1))
             else:
                 if n == W:
                     torch.cuda.synchronize(self.device)
                     tr[2] = time.perf_counter()
                 self.engine.replay_begin()
-                self._graph.replay()
+                self._on_graph_stream(self._graph.replay)
                 self.engine.replay_end()
                 if n == W + K - 1:
                     torch.cuda.synchronize(self.device)
                     graph_ms = (time.perf_counter() - tr[2]) / K * 1e3
+                    # every rank decides from the slowest rank's timings (the same mode everywhere)
+                    tr[3], graph_ms = agree_ms([tr[3], graph_ms], getattr(self.engine, "group", None))
                     keep = graph_ms < tr[3]
                     self.graph_choice = {"eager_ms": round(tr[3], 3), "graph_ms": round(graph_ms, 3),
                                          "mode": "segmented graphs" if keep else "eager"}
@@ -306,6 +353,7 @@ class TrainingSession:
             self._graph = side_graph
             return
         side_ms, one_ms = min(tr[3], ms), tr[6]
+        side_ms, one_ms = agree_ms([side_ms, one_ms], getattr(self.engine, "group", None))  # same choice on every rank
         keep = one_ms < 0.97 * side_ms   # (a clear win only: a host-bound loop times both alike)
         self.side_choice = {"side_ms": round(side_ms, 3), "one_stream_ms": round(one_ms, 3),
                             "mode": "one stream" if keep else "weight-gradient side stream"}
@@ -350,9 +398,10 @@ class TrainingSession:
         # the host load of batch k+1 runs on a worker thread while this thread enqueues step k
         # (a graph launch blocks the caller ~1 ms for a CIFAR step; the feeder's staging copies
         # wait on the event that ends the consumption of the previous batch, so they are
-        # stream-ordered whichever thread issues them); DRN_ASYNC_PREFETCH=0: inline after the step
+        # stream-ordered whichever thread issues them). A step that captures a graph gets its
+        # prefetch inline after it: no second thread may allocate or synchronize during a capture
         pool = None
-        if prefetch is not None and self.device.type == "cuda" and os.environ.get("DRN_ASYNC_PREFETCH", "1") == "1":
+        if prefetch is not None and self.device.type == "cuda":
             from concurrent.futures import ThreadPoolExecutor
             pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="drn-prefetch")
         pending = None
@@ -367,10 +416,11 @@ class TrainingSession:
                 self.data_state = feeder.state()
                 for h in hooks:
                     h.before_step(self, self.global_step)
-                if pool is not None:
+                capture = self.will_capture()
+                if pool is not None and not capture:
                     pending = pool.submit(prefetch)
                 self.step()
-                if prefetch is not None and pool is None:
+                if prefetch is not None and (pool is None or capture):
                     # the host loads batch k+1 while the GPU runs step k (enqueued above)
                     with phase("data prefetch"):
                         prefetch()

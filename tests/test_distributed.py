@@ -204,3 +204,34 @@ def test_sharded_optimizer_matches_allreduce_dp(world):
     for rank, ew, em in res:
         assert isinstance(ew, float), ew
         assert ew < 1e-6 and em < 1e-5, (rank, ew, em)
+
+
+def _agree_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from distributed_resnet_tensorflow_amd.train.session import agree_ms
+        # rank 0 measured the eager step faster, rank 1 the graph step: alone they would split
+        mine = [10.0, 11.0] if rank == 0 else [12.0, 9.5]
+        eager_ms, graph_ms = agree_ms(mine)
+        q.put((rank, eager_ms, graph_ms, "graph" if graph_ms < eager_ms else "eager"))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, "error", repr(e), None))
+
+
+def test_step_mode_trial_agrees_across_ranks():
+    """The session's timing trials (eager vs segmented graphs, side stream vs one stream) decide
+    from the slowest rank's timings (train/session.py agree_ms): two ranks whose own timings
+    disagree take the SAME step mode."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_agree_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    assert all(o[1] != "error" for o in out), out
+    assert out[0][1:] == out[1][1:] == (12.0, 11.0, "graph"), out

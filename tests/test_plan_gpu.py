@@ -1,0 +1,137 @@
+"""Native step plans (runtime/plan.py, csrc/kernels/plan.hip): a training step recorded once and
+replayed from C++ must do exactly what the eager Python step does.
+
+  * bitwise: in the deterministic mode (DRN_DETERMINISTIC=1: no float atomics anywhere) an
+    executor trained by 1 eager step + 3 plan replays ends with the same weights, momentum and BN
+    moving statistics, bit for bit, as one trained by 4 eager steps -- with the weight-gradient
+    side stream, its cross-stream events, the deferred stem tail and the carried-over data-
+    gradient weight refresh all replayed natively;
+  * data parallel: the same on a single-rank process group (gloo, GPU tensors), the plan cut at
+    every bucket report with the collectives issued from Python between native segments;
+  * the plan replaces hundreds of Python launches by a handful of host calls.
+"""
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")]
+
+
+def _ex(seed=3, N=8, dp=False):
+    from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2
+    from distributed_resnet_tensorflow_amd.ops.backend import HipBackend
+    from distributed_resnet_tensorflow_amd.runtime.executor import Executor
+    ex = Executor(cifar_resnet_v2(8), N, HipBackend("cuda"), "cuda", seed=seed)
+    g = torch.Generator().manual_seed(7)
+    ex.images.zero_()
+    ex.images[..., :3] = torch.randn(N, 32, 32, 3, generator=g).bfloat16().cuda()
+    ex.labels.copy_(torch.randint(0, 10, (N,), generator=g, dtype=torch.int32))
+    ex.set_lr(0.05)
+    return ex
+
+
+def _state(ex):
+    torch.cuda.synchronize()
+    return [t.clone() for t in (ex.P.master, ex.P.momentum, ex.P.bn_state, ex.P.wbf16)]
+
+
+def _eager_step(ex, eng=None):
+    ex.forward(train=True)
+    if eng is None:
+        ex.backward(defer_tail=True)
+        ex.apply_gradients()
+    else:
+        eng.begin_step()
+        ex.backward()
+        eng.apply_gradients(eng.finish(), 1.0)
+
+
+def test_plan_replay_bitwise_equals_eager(monkeypatch):
+    monkeypatch.setenv("DRN_DETERMINISTIC", "1")
+    from distributed_resnet_tensorflow_amd.runtime.plan import StepPlan
+    a = _ex()
+    assert a.side is not None   # the weight-gradient side stream and its events are part of the plan
+    for _ in range(4):
+        _eager_step(a)
+    want = _state(a)
+    b = _ex()
+    plan = StepPlan(b, warmup=1)   # = 1 eager step, then the recording (which executes nothing)
+    for _ in range(3):
+        plan.replay()
+    got = _state(b)
+    for name, x, y in zip(("master", "momentum", "bn_state", "wbf16"), got, want):
+        assert torch.equal(x, y), name
+    assert plan.launches > 100 and len(plan.cuts) == 1
+
+
+def test_plan_replay_side_stream_and_deferred_tail_nondeterministic():
+    """Default (autotuned, atomics allowed) mode on the ImageNet topology at a small shape: the
+    replayed steps train like the eager ones (same loss trajectory to rounding)."""
+    from distributed_resnet_tensorflow_amd.models.spec import imagenet_resnet_v2
+    from distributed_resnet_tensorflow_amd.ops.backend import HipBackend
+    from distributed_resnet_tensorflow_amd.runtime.executor import Executor
+    from distributed_resnet_tensorflow_amd.runtime.plan import StepPlan
+    losses = {}
+    for mode in ("eager", "plan"):
+        be = HipBackend("cuda")
+        ex = Executor(imagenet_resnet_v2(50, num_classes=11, image_size=64), 4, be, "cuda", seed=5, weight_decay=1e-4)
+        be.synthetic_images(ex.images, seed=9)
+        ex.labels.copy_(torch.arange(4, dtype=torch.int32))
+        ex.set_lr(0.02)
+        ex.autotune()
+        out = []
+        if mode == "eager":
+            for _ in range(5):
+                _eager_step(ex)
+                torch.cuda.synchronize()
+                out.append(float(ex.loss_vec.float().mean()))
+        else:
+            plan = StepPlan(ex, warmup=1)
+            torch.cuda.synchronize()
+            out.append(float(ex.loss_vec.float().mean()))
+            for _ in range(4):
+                plan.replay()
+                torch.cuda.synchronize()
+                out.append(float(ex.loss_vec.float().mean()))
+        losses[mode] = out
+    for x, y in zip(losses["plan"], losses["eager"]):
+        assert abs(x - y) <= 2e-3 * max(1.0, abs(y)), losses
+    assert losses["plan"][-1] < losses["plan"][0], losses   # it trains
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_plan_replay_data_parallel_bitwise(monkeypatch):
+    monkeypatch.setenv("DRN_DETERMINISTIC", "1")
+    import torch.distributed as dist
+    from distributed_resnet_tensorflow_amd.parallel.engine import DataParallelEngine
+    from distributed_resnet_tensorflow_amd.runtime.plan import StepPlan
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        res = []
+        for mode in ("eager", "plan"):
+            ex = _ex(seed=11)
+            eng = DataParallelEngine(ex, bucket_mb=0.05, allreduce="rccl")
+            assert len(eng.buckets) > 2 and eng.p2p is None
+            if mode == "eager":
+                for _ in range(4):
+                    _eager_step(ex, eng)
+            else:
+                plan = StepPlan(ex, eng, grad_scale=1.0, warmup=1)
+                assert sum(1 for _, a in plan.cuts if isinstance(a, tuple)) >= 2   # cut at the reports
+                for _ in range(3):
+                    plan.replay()
+            res.append(_state(ex))
+        for name, x, y in zip(("master", "momentum", "bn_state", "wbf16"), res[1], res[0]):
+            assert torch.equal(x, y), name
+    finally:
+        dist.destroy_process_group()

@@ -62,3 +62,46 @@ def test_p2p_dp_graph_step_side_stream_trial(monkeypatch):
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
+
+
+def test_graph_step_staged_feeder_async_prefetch(tmp_path):
+    """The real CIFAR input path under graph steps: staged feeder (pinned loader, H2D copies on
+    the feeder's stream), the host prefetch of batch k+1 on the session's worker thread while
+    step k is enqueued -- except around the steps that capture a graph (the first step and the
+    side-stream trial's re-capture: TrainingSession.will_capture) -- and every step consumes
+    the loader's batches in order (feeder prefetch vs graph capture)."""
+    import numpy as np
+    from distributed_resnet_tensorflow_amd.data import cifar
+    from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2
+    from distributed_resnet_tensorflow_amd.parallel.cluster import ClusterInfo
+    from distributed_resnet_tensorflow_amd.train import lr as lr_mod
+    from distributed_resnet_tensorflow_amd.train.feeder import CifarFeeder
+    from distributed_resnet_tensorflow_amd.train.hooks import Hook, StopAtStepHook
+    from distributed_resnet_tensorflow_amd.train.session import TrainingSession
+    cifar.write_fake_cifar(str(tmp_path), 120)
+    rec = cifar.CifarRecords(cifar.get_filenames(True, str(tmp_path)))
+    N, steps = 32, 40
+    ref_ld = cifar.CifarLoader(rec, N, True, seed=7)
+    ref = [np.array(next(ref_ld)[1], copy=True) for _ in range(steps)]
+    ref_ld.close()
+    sess = TrainingSession(cifar_resnet_v2(8), N, ClusterInfo(device="cuda:0"), weight_decay=2e-4,
+                           lr_schedule=lr_mod.for_dataset("cifar10"), use_graph=True)
+    captures = []
+    hist = torch.empty(steps, N, dtype=torch.int32, device="cuda")
+
+    class Record(Hook):
+        def before_step(self, s, step):
+            captures.append(s.will_capture())
+
+        def after_step(self, s, step, metrics):
+            hist[step - 1].copy_(s.ex.labels)
+
+    feeder = CifarFeeder(sess.ex, cifar.CifarLoader(rec, N, True, seed=7, pin=True, pin_device=sess.ex.device), True)
+    sess.run(feeder, [StopAtStepHook(steps), Record()])
+    feeder.close()
+    torch.cuda.synchronize()
+    assert sess.global_step == steps and sess.failed is None
+    assert captures[0] and sum(captures) >= 2, captures   # first capture + the trial's re-capture
+    for k in range(steps):
+        np.testing.assert_array_equal(hist[k].cpu().numpy(), ref[k], err_msg=f"labels of step {k}")
+    assert float(sess.ex.metrics()["cross_entropy"]) == float(sess.ex.metrics()["cross_entropy"])
