@@ -13,7 +13,8 @@
 // LDS, stream, by-value argument copy} instead of launching (drn_common.h), and the runtime adds
 // event-record / stream-wait entries (drn_plan_event_record / drn_plan_stream_wait) where the
 // Python step would have called torch's stream API. drn_plan_replay(begin, end) then re-issues
-// entries [begin, end) with hipLaunchKernel / hipEventRecord / hipStreamWaitEvent: the same
+// entries [begin, end) with hipModuleLaunchKernel (function handles resolved at record time) /
+// hipEventRecord / hipStreamWaitEvent: the same
 // kernels, arguments, streams and priorities as the eager step, one host call per segment (the
 // data-parallel step is cut at the points where a bucket collective is issued from Python).
 // The equivalent of the reference's per-step `mon_sess.run(train_op)` executor call
@@ -31,6 +32,7 @@ struct PlanEntry {
   enum Kind : int { LAUNCH = 0, RECORD = 1, WAIT = 2 };
   int kind = LAUNCH;
   const void* fn = nullptr;
+  hipFunction_t func = nullptr;  // resolved once at record time: replay skips the stub lookup
   dim3 grid, block;
   size_t shm = 0;
   hipStream_t stream = nullptr;
@@ -58,6 +60,7 @@ void plan_add_launch(Plan* p, const void* fn, dim3 grid, dim3 block, size_t shm,
   PlanEntry x;
   x.kind = PlanEntry::LAUNCH;
   x.fn = fn;
+  if (hipGetFuncBySymbol(&x.func, fn) != hipSuccess) x.func = nullptr;
   x.grid = grid;
   x.block = block;
   x.shm = shm;
@@ -137,7 +140,9 @@ DRN_API int drn_plan_replay(void* pv, int begin, int end) {
     hipError_t rc;
     switch (x.kind) {
       case PlanEntry::LAUNCH:
-        rc = hipLaunchKernel(x.fn, x.grid, x.block, x.argv, x.shm, x.stream);
+        rc = x.func != nullptr ? hipModuleLaunchKernel(x.func, x.grid.x, x.grid.y, x.grid.z, x.block.x, x.block.y,
+                                                       x.block.z, (unsigned)x.shm, x.stream, x.argv, nullptr)
+                               : hipLaunchKernel(x.fn, x.grid, x.block, x.argv, x.shm, x.stream);
         break;
       case PlanEntry::RECORD:
         rc = hipEventRecord(p->events[x.ev], x.stream);

@@ -20,6 +20,7 @@ from ..ops.backend import HipBackend, RefBackend
 from ..parallel.engine import DataParallelEngine
 from ..runtime.executor import Executor
 from ..runtime.graph import SegmentedStepGraph, StepGraph
+from ..runtime.plan import StepPlan
 from ..runtime.state import export_state, import_state
 from ..utils.profiler import enable_phases, phase
 from .hooks import Hook
@@ -119,17 +120,20 @@ class TrainingSession:
         # collective is a kernel with device-side flags): also the whole step, comm included, in
         # one graph. Data parallel over RCCL: the chain of per-segment graphs
         # (SegmentedStepGraph) or eager, whichever the first steps measure faster
-        # (DRN_DP_GRAPH=auto, the default; 1 / 0 force one): ImageNet ResNet-50 runs faster
-        # eager (side-stream weight gradients), CIFAR steps are launch-bound eager (~260 Python
-        # launches for a ~2 ms step) and run faster as graphs
+        # or the native step plan (runtime/plan.py: the eager step replayed from C++, the bucket
+        # collectives issued from Python at its cut points), whichever the first steps measure
+        # fastest (DRN_DP_GRAPH=auto, the default; 1 / 0 force graphs / eager): ImageNet ResNet-50
+        # runs fastest with the eager structure (side-stream weight gradients), CIFAR steps are
+        # launch-bound in Python (~260 launches for a ~2 ms step)
         dp_ok = dp and self.engine.mode == "sync" and not self.sharded
         dp_graph = os.environ.get("DRN_DP_GRAPH", "auto")
         hip_cuda = self.device.type == "cuda" and self.be.name == "hip"
         self.use_graph = use_graph and hip_cuda and (
             not dp or (dp_ok and self.engine.p2p is not None) or (dp_ok and dp_graph == "1"))
-        # eager-vs-segmented-graph trial: [phase, steps in phase, t0, eager ms/step]
-        self._trial = ["eager", 0, 0.0, 0.0] if (use_graph and hip_cuda and dp_ok and self.engine.p2p is None
-                                                and dp_graph == "auto") else None
+        # step-mode trial of the RCCL data-parallel step: eager, native plan, segmented graphs
+        self._trial = {"modes": ["eager", "plan", "graph"], "i": 0, "n": 0, "t0": 0.0, "ms": {}} \
+            if (use_graph and hip_cuda and dp_ok and self.engine.p2p is None and dp_graph == "auto") else None
+        self._plan: Optional[StepPlan] = None
         self.graph_choice: Optional[dict] = None
         # single-GPU graph step: its first replays time the step with and without the weight-
         # gradient side stream and keep the faster (CIFAR ResNet-50 bs32: one stream 1.585 ms vs
@@ -216,7 +220,8 @@ class TrainingSession:
             return False
         if self.use_graph and (self._graph is None or (isinstance(self._graph, _LazyGraph) and self._graph.g is None)):
             return True
-        return self._trial is not None and self._trial[0] == "graph" and self._graph is None
+        tr = self._trial
+        return tr is not None and tr["modes"][tr["i"]] == "graph" and self._graph is None
 
     def _step_body(self):
         ex = self.ex
@@ -264,6 +269,8 @@ class TrainingSession:
                     self._side_trial_tick()
         elif self._trial is not None and not self.ex.check_nan:
             self._trial_step()
+        elif self._plan is not None and not self.ex.check_nan:
+            self._plan.replay()
         else:
             self._step_body()
         self.lr.after_step(self.ex.P.global_step)
@@ -275,53 +282,65 @@ class TrainingSession:
     TRIAL_WARM, TRIAL_STEPS = 3, 10
 
     def _trial_step(self):
-        """One REAL training step of the eager-vs-segmented-graph trial (data parallel over
-        RCCL): TRIAL_WARM + TRIAL_STEPS eager steps, then the graph is built (its construction
-        runs this step eagerly and captures it), TRIAL_WARM + TRIAL_STEPS replays; the faster
-        mode stays. Both modes launch the same kernels in the same order on the same buffers:
-        the choice changes the step time, not the numerics."""
+        """One REAL training step of the step-mode trial (data parallel over RCCL): per mode --
+        eager, native plan, segmented graphs -- TRIAL_WARM + TRIAL_STEPS steps (a plan's or a
+        graph's construction step runs the step eagerly first and is one of them); the fastest
+        mode by the slowest rank's timings stays on every rank. Every mode launches the same
+        kernels in the same order on the same buffers: the choice changes the step time, not the
+        numerics. Mode switches synchronize the device (each mode orders its own cross-stream
+        events)."""
         tr = self._trial
-        ph, n = tr[0], tr[1]
+        mode = tr["modes"][tr["i"]]
         W, K = self.TRIAL_WARM, self.TRIAL_STEPS
-        if ph == "eager":
-            if n == W:
-                torch.cuda.synchronize(self.device)
-                tr[2] = time.perf_counter()
-            self._step_body()
-            if n == W + K - 1:
-                torch.cuda.synchronize(self.device)
-                tr[3] = (time.perf_counter() - tr[2]) / K * 1e3
-                tr[0], tr[1] = "graph", -1
-                return
+        if mode == "plan" and self._plan is None:
+            torch.cuda.synchronize(self.device)
+            self._plan = StepPlan(self.ex, self.engine, 1.0 / self.world, warmup=1)
+            return
+        if mode == "graph" and self._graph is None:
+            torch.cuda.synchronize(self.device)
+            self._graph = self._on_graph_stream(
+                lambda: SegmentedStepGraph(self.ex, self.engine, 1.0 / self.world, warmup=1))
+            return
+        n = tr["n"]
+        if n == W:
+            torch.cuda.synchronize(self.device)
+            tr["t0"] = time.perf_counter()
+        self._run_mode(mode)
+        if n < W + K - 1:
+            tr["n"] = n + 1
+            return
+        torch.cuda.synchronize(self.device)
+        tr["ms"][mode] = (time.perf_counter() - tr["t0"]) / K * 1e3
+        tr["i"], tr["n"] = tr["i"] + 1, 0
+        if tr["i"] < len(tr["modes"]):
+            return
+        modes = tr["modes"]
+        ms = agree_ms([tr["ms"][m] for m in modes], getattr(self.engine, "group", None))  # same mode everywhere
+        pick = modes[min(range(len(modes)), key=lambda i: ms[i])]
+        self.graph_choice = {f"{m}_ms": round(v, 3) for m, v in zip(modes, ms)}
+        self.graph_choice["mode"] = {"graph": "segmented graphs", "plan": "native plan"}.get(pick, "eager")
+        log.info("data-parallel step: %s -> %s", ", ".join(f"{m} {v:.3f} ms" for m, v in zip(modes, ms)),
+                 self.graph_choice["mode"])
+        torch.cuda.synchronize(self.device)
+        if pick != "graph":   # back to the eager structure: drop the graphs, weight gradients on the side stream
+            self.ex.side = self._graph.side_stream
+            self._graph = None
         else:
-            if self._graph is None:
-                self._graph = self._on_graph_stream(
-                    lambda: SegmentedStepGraph(self.ex, self.engine, 1.0 / self.world, warmup=1))
-            else:
-                if n == W:
-                    torch.cuda.synchronize(self.device)
-                    tr[2] = time.perf_counter()
-                self.engine.replay_begin()
-                self._on_graph_stream(self._graph.replay)
-                self.engine.replay_end()
-                if n == W + K - 1:
-                    torch.cuda.synchronize(self.device)
-                    graph_ms = (time.perf_counter() - tr[2]) / K * 1e3
-                    # every rank decides from the slowest rank's timings (the same mode everywhere)
-                    tr[3], graph_ms = agree_ms([tr[3], graph_ms], getattr(self.engine, "group", None))
-                    keep = graph_ms < tr[3]
-                    self.graph_choice = {"eager_ms": round(tr[3], 3), "graph_ms": round(graph_ms, 3),
-                                         "mode": "segmented graphs" if keep else "eager"}
-                    log.info("data-parallel step: eager %.3f ms, segmented graphs %.3f ms -> %s", tr[3], graph_ms,
-                             self.graph_choice["mode"])
-                    if keep:
-                        self.use_graph = True
-                    else:  # back to eager: drop the graphs, weight gradients back on the side stream
-                        self.ex.side = self._graph.side_stream
-                        self._graph = None
-                    self._trial = None
-                    return
-        tr[1] = n + 1
+            self.use_graph = True
+        if pick != "plan":
+            self._plan = None
+        self._mode = pick
+        self._trial = None
+
+    def _run_mode(self, mode: str):
+        if mode == "eager":
+            self._step_body()
+        elif mode == "plan":
+            self._plan.replay()
+        else:
+            self.engine.replay_begin()
+            self._on_graph_stream(self._graph.replay)
+            self.engine.replay_end()
 
     def _side_trial_tick(self):
         """After each REAL graph-replayed step of the side-stream trial, in three timed phases of

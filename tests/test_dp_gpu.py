@@ -277,8 +277,9 @@ def _schedule_worker(backend, port, q):
         launch = eng._launch
 
         def rec(i, buf=None):
-            # (bucket, frontier when it fired, stream it was issued from)
-            side = ex.side is not None and torch.cuda.current_stream() == ex.side
+            # (bucket, frontier when it fired, issued from the report stream: ordered by the
+            # per-bucket readiness events of both compute streams, neither of them waiting)
+            side = ex._report_stream is not None and torch.cuda.current_stream() == ex._report_stream
             log.append((i, eng.frontier, side))
             return launch(i, buf)
         eng._launch = rec
@@ -298,7 +299,7 @@ def _schedule_worker(backend, port, q):
 
 def test_rccl_engine_bucket_schedule_matches_gloo():
     """The RCCL (torch "nccl") engine issues the same buckets at the same backward positions, from
-    the weight-gradient side stream, as the gloo engine the multi-rank CPU/GPU rehearsals use: the
+    the executor's report stream, as the gloo engine the multi-rank CPU/GPU rehearsals use: the
     N>1 production path differs from the rehearsed one only in the transport."""
     ctx = mp.get_context("spawn")
     res = {}
@@ -314,7 +315,7 @@ def test_rccl_engine_bucket_schedule_matches_gloo():
     assert bn == bg and len(bn) > 2
     assert ln == lg
     assert len(ln) == 2 * len(bn)                      # every bucket once per step
-    assert all(side for _, _, side in ln[:-1])         # issued from the side stream (not the last,
+    assert all(side for _, _, side in ln[:-1])         # issued from the report stream (not the last,
                                                        # which finish() issues on the main stream)
     # same numbers up to the two processes' independent (timing-based) kernel autotuning and the
     # fp32-atomic accumulation order: two steps apart by ~1e-3 relative (seen up to 2.2e-3)
@@ -334,31 +335,33 @@ def _trial_worker(port, q, mode):
         sess = TrainingSession(cifar_resnet_v2(8), 32, ClusterInfo(device="cuda:0"), weight_decay=2e-4,
                                lr_schedule=lr_mod.for_dataset("cifar10"), use_graph=True, allreduce="rccl")
         assert sess.engine is not None and sess.engine.p2p is None and not sess.use_graph
-        sess.run(SyntheticFeeder(sess.ex, seed=0), [StopAtStepHook(40)])
+        sess.run(SyntheticFeeder(sess.ex, seed=0), [StopAtStepHook(60)])
         loss = float(sess.ex.metrics()["cross_entropy"])
-        q.put((mode, sess.graph_choice, sess.global_step, sess.use_graph, sess.ex.side is not None, loss))
+        q.put((mode, sess.graph_choice, sess.global_step, sess.use_graph, sess.ex.side is not None, loss,
+               sess._plan is not None))
     except Exception as e:  # pragma: no cover
         import traceback
-        q.put((mode, repr(e) + traceback.format_exc(), None, None, None, None))
+        q.put((mode, repr(e) + traceback.format_exc(), None, None, None, None, None))
 
 
 @pytest.mark.timeout(300)
-def test_rccl_dp_session_times_eager_vs_segmented_graphs():
+def test_rccl_dp_session_times_eager_plan_and_segmented_graphs():
     """Data parallel over RCCL (single-rank process group): the session's first steps time the
-    eager step and the chain of segmented graphs, keep the faster, and keep training in that mode
-    (DRN_DP_GRAPH=auto); DRN_DP_GRAPH=0 stays eager with no trial."""
+    eager step, the native step plan and the chain of segmented graphs, keep the fastest, and keep
+    training in that mode (DRN_DP_GRAPH=auto); DRN_DP_GRAPH=0 stays eager with no trial."""
     ctx = mp.get_context("spawn")
     for mode in ("auto", "0"):
         q = ctx.Queue()
         p = ctx.Process(target=_trial_worker, args=(_free_port(), q, mode))
         p.start()
-        m, choice, step, graph, side, loss = q.get(timeout=280)
+        m, choice, step, graph, side, loss, plan = q.get(timeout=280)
         p.join(timeout=60)
         assert not isinstance(choice, str), choice
-        assert step == 40 and loss == loss, (step, loss)
+        assert step == 60 and loss == loss, (step, loss)
         if mode == "auto":
-            assert choice is not None and choice["eager_ms"] > 0 and choice["graph_ms"] > 0, choice
+            assert choice is not None and min(choice["eager_ms"], choice["plan_ms"], choice["graph_ms"]) > 0, choice
             assert graph == (choice["mode"] == "segmented graphs")
-            assert side == (not graph)  # eager keeps the weight-gradient side stream
+            assert plan == (choice["mode"] == "native plan")
+            assert side == (not graph)  # eager and the plan keep the weight-gradient side stream
         else:
-            assert choice is None and not graph and side
+            assert choice is None and not graph and side and not plan

@@ -63,7 +63,7 @@ def test_plan_replay_bitwise_equals_eager(monkeypatch):
     got = _state(b)
     for name, x, y in zip(("master", "momentum", "bn_state", "wbf16"), got, want):
         assert torch.equal(x, y), name
-    assert plan.launches > 100 and len(plan.cuts) == 1
+    assert plan.launches > 50 and len(plan.cuts) == 1, (plan.launches, plan.cuts)
 
 
 def test_plan_replay_side_stream_and_deferred_tail_nondeterministic():
