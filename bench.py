@@ -194,7 +194,7 @@ def main():
     if eng is not None and eng.zero1:
         use_graph = 0
     want_plan = args.plan != 0 and (eng is None or (eng.p2p is None and not eng.zero1 and eng.mode == "sync"))
-    cands, mode_times = {}, None
+    cands, mode_times, plan = {}, None, None
 
     def in_eager_ctx(fn):
         if prio is None:
@@ -217,6 +217,19 @@ def main():
         cands["plan"] = in_eager_ctx(plan.replay)
         if args.plan == 1:
             cands.pop("eager", None)
+        if ex.side is not None:
+            # the same plan issued by one host thread per stream (StepPlan.set_threads)
+            def plan_mt():
+                if plan.threads != 2:
+                    plan.set_threads(2)
+                plan.replay()
+
+            def plan_1t():
+                if plan.threads != 1:
+                    plan.set_threads(1)
+                plan.replay()
+            cands["plan"] = in_eager_ctx(plan_1t)
+            cands["plan_threads"] = in_eager_ctx(plan_mt)
     mode = next(iter(cands))
     if len(cands) > 1:
         mode, mode_times = _pick(cands)
@@ -234,7 +247,8 @@ def main():
         mode_times = {**(mode_times or {}), **t1}
     run = cands[mode]
     use_graph = int(mode in ("graph", "graph_one_stream", "segmented"))
-    # host enqueue time of one step of the chosen mode (from an idle queue: nothing blocks)
+    # host enqueue time of the chosen mode: one step from an idle queue (nothing blocks), and
+    # the median over the timed steps (host time per run() call)
     torch.cuda.synchronize()
     t_host = time.perf_counter()
     run()
@@ -246,9 +260,12 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    t_calls = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        tc = time.perf_counter()
         run()
+        t_calls.append(time.perf_counter() - tc)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -301,7 +318,10 @@ def main():
                        "wgrad_side_stream": ex.side is not None},
             "final_loss": round(loss, 4),
             "host_enqueue_ms": round(t_host, 3),
+            "host_call_ms_median": round(sorted(t_calls)[len(t_calls) // 2] * 1e3, 3),
         }
+        if plan is not None and mode.startswith("plan"):
+            out["plan"] = plan.stats()
         if mode_times is not None:
             out["mode_trial_ms"] = mode_times
         if dp is not None:

@@ -150,6 +150,9 @@ _SIGS = {
     "drn_plan_size": ([c_p], c_int),
     "drn_plan_launches": ([c_p], c_int),
     "drn_plan_replay": ([c_p, c_int, c_int], c_int),
+    "drn_plan_set_threads": ([c_p, c_int], c_int),
+    "drn_plan_lanes": ([c_p], c_int),
+    "drn_plan_count": ([c_p, c_int], c_int),
 }
 
 

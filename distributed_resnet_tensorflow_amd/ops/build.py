@@ -168,7 +168,7 @@ def build(force: bool = False, verbose: bool = True, extra: list[str] | None = N
             print(f"[drn.build] up to date: {LIB_PATH}")
         return LIB_PATH
     tmp = LIB_PATH.with_suffix(".so.tmp")
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + [str(o) for o in objs]
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", "-o", str(tmp)] + [str(o) for o in objs]
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
         raise RuntimeError(f"link failed:\n{res.stderr[-6000:]}")

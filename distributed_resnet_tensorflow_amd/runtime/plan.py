@@ -113,7 +113,7 @@ class StepPlan:
     update) recorded after one eager warm-up step, replayed natively. The caller keeps the
     stream context it recorded under (the recorded launches name their streams explicitly)."""
 
-    def __init__(self, ex, engine=None, grad_scale: float = 1.0, warmup: int = 1):
+    def __init__(self, ex, engine=None, grad_scale: float = 1.0, warmup: int = 1, threads: int = 1):
         self.L = _lib.lib()
         self.ex, self.eng, self.grad_scale = ex, engine, grad_scale
         if engine is not None and (engine.p2p is not None or engine.mode != "sync" or engine.zero1):
@@ -153,7 +153,21 @@ class StepPlan:
         # them through torch (mixing eager steps and replays needs a device synchronize)
         ex._tflip_ev = ex._tail_ev = ex._stem_ev = None
         self.launches = int(self.L.drn_plan_launches(self.p))
+        self.set_threads(threads)
         torch.cuda.synchronize()
+
+    def set_threads(self, n: int):
+        """Host threads issuing a replay: 1 = the calling thread, in recorded order; n > 1 = one
+        thread per stream (the critical-path and weight-gradient streams' launches enqueued
+        concurrently, cross-stream events in recorded order; csrc/kernels/plan.hip)."""
+        _lib.check(self.L.drn_plan_set_threads(self.p, int(n)), "drn_plan_set_threads")
+        self.threads = int(n)
+
+    def stats(self) -> dict:
+        L, p = self.L, self.p
+        return {"launches": self.launches, "event_records": int(L.drn_plan_count(p, 1)),
+                "stream_waits": int(L.drn_plan_count(p, 2)), "streams": int(L.drn_plan_lanes(p)),
+                "segments": sum(1 for _, a in self.cuts if a is not None) + 1, "threads": self.threads}
 
     def _eager(self):
         ex, eng = self.ex, self.eng

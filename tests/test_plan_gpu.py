@@ -48,7 +48,10 @@ def _eager_step(ex, eng=None):
         eng.apply_gradients(eng.finish(), 1.0)
 
 
-def test_plan_replay_bitwise_equals_eager(monkeypatch):
+@pytest.mark.parametrize("threads", [1, 2])
+def test_plan_replay_bitwise_equals_eager(monkeypatch, threads):
+    """threads = 2: one host thread per stream issues the replay (cross-stream events in
+    recorded order)."""
     monkeypatch.setenv("DRN_DETERMINISTIC", "1")
     from distributed_resnet_tensorflow_amd.runtime.plan import StepPlan
     a = _ex()
@@ -57,7 +60,8 @@ def test_plan_replay_bitwise_equals_eager(monkeypatch):
         _eager_step(a)
     want = _state(a)
     b = _ex()
-    plan = StepPlan(b, warmup=1)   # = 1 eager step, then the recording (which executes nothing)
+    plan = StepPlan(b, warmup=1, threads=threads)   # = 1 eager step, then the recording (executes nothing)
+    assert plan.stats()["streams"] >= 2
     for _ in range(3):
         plan.replay()
     got = _state(b)
@@ -68,7 +72,12 @@ def test_plan_replay_bitwise_equals_eager(monkeypatch):
 
 def test_plan_replay_side_stream_and_deferred_tail_nondeterministic():
     """Default (autotuned, atomics allowed) mode on the ImageNet topology at a small shape: the
-    replayed steps train like the eager ones (same loss trajectory to rounding)."""
+    replayed steps train like the eager ones. Not a rounding-level comparison: the BN-statistics
+    atomics make even two eager runs differ, and at 4 images x 64 px (16 rows per stage-4 BN
+    channel) a one-ulp difference in block 1 grows to ~20 % at the logits (repeated forwards
+    from one state give bitwise-equal or such amplified losses: scripts/fwd_repeatability.py,
+    profiles/r5_fwd_repeatability.txt). The bitwise tests above pin the replay semantics in the
+    deterministic mode."""
     from distributed_resnet_tensorflow_amd.models.spec import imagenet_resnet_v2
     from distributed_resnet_tensorflow_amd.ops.backend import HipBackend
     from distributed_resnet_tensorflow_amd.runtime.executor import Executor
@@ -96,9 +105,10 @@ def test_plan_replay_side_stream_and_deferred_tail_nondeterministic():
                 torch.cuda.synchronize()
                 out.append(float(ex.loss_vec.float().mean()))
         losses[mode] = out
-    for x, y in zip(losses["plan"], losses["eager"]):
-        assert abs(x - y) <= 2e-3 * max(1.0, abs(y)), losses
-    assert losses["plan"][-1] < losses["plan"][0], losses   # it trains
+    assert losses["plan"][0] == losses["eager"][0] or abs(losses["plan"][0] - losses["eager"][0]) < 0.15, losses
+    assert abs(losses["plan"][1] - losses["eager"][1]) <= 0.25 * losses["eager"][1], losses
+    for mode in ("eager", "plan"):   # both train (the synthetic batch is memorised within 5 steps)
+        assert losses[mode][-1] < 0.5 * losses[mode][0], losses
 
 
 def _free_port():
@@ -109,7 +119,8 @@ def _free_port():
     return p
 
 
-def test_plan_replay_data_parallel_bitwise(monkeypatch):
+@pytest.mark.parametrize("threads", [1, 2])
+def test_plan_replay_data_parallel_bitwise(monkeypatch, threads):
     monkeypatch.setenv("DRN_DETERMINISTIC", "1")
     import torch.distributed as dist
     from distributed_resnet_tensorflow_amd.parallel.engine import DataParallelEngine
@@ -126,7 +137,7 @@ def test_plan_replay_data_parallel_bitwise(monkeypatch):
                 for _ in range(4):
                     _eager_step(ex, eng)
             else:
-                plan = StepPlan(ex, eng, grad_scale=1.0, warmup=1)
+                plan = StepPlan(ex, eng, grad_scale=1.0, warmup=1, threads=threads)
                 assert sum(1 for _, a in plan.cuts if isinstance(a, tuple)) >= 2   # cut at the reports
                 for _ in range(3):
                     plan.replay()
