@@ -204,11 +204,18 @@ def main():
                 fn()
         return f
 
+    one_stream = {}   # modes recorded / captured without the weight-gradient side stream
     if use_graph and eng is not None and eng.p2p is None:
         cands["segmented"] = SegmentedStepGraph(ex, eng, 1.0 / world, warmup=1).replay
     elif use_graph:
-        sg = StepGraph(step, warmup=2)
-        cands["graph"] = sg.replay
+        cands["graph"] = StepGraph(step, warmup=2).replay
+        if ex.side is not None and args.graph == -1:
+            # the graph without the weight-gradient side stream (one stream: CIFAR ResNet-50 bs32
+            # 1.585 vs 1.785 ms; the side stream wins for larger steps)
+            side, ex.side = ex.side, None
+            cands["graph_one_stream"] = StepGraph(step, warmup=2).replay
+            ex.side = side
+            one_stream["graph_one_stream"] = True
     if args.graph != 1 or not cands:
         cands["eager"] = eager
     if want_plan and (args.plan == 1 or "eager" in cands):
@@ -230,21 +237,19 @@ def main():
                 plan.replay()
             cands["plan"] = in_eager_ctx(plan_1t)
             cands["plan_threads"] = in_eager_ctx(plan_mt)
+            if eng is None and args.plan != 1:
+                # ... and a plan recorded without the side stream (small steps)
+                side, ex.side = ex.side, None
+                with torch.cuda.stream(prio) if prio is not None else torch.cuda.stream(torch.cuda.current_stream()):
+                    plan1 = StepPlan(ex, None, warmup=1)
+                ex.side = side
+                cands["plan_one_stream"] = in_eager_ctx(plan1.replay)
+                one_stream["plan_one_stream"] = True
     mode = next(iter(cands))
     if len(cands) > 1:
         mode, mode_times = _pick(cands)
-    if mode == "graph" and (eng is None or eng.p2p is not None) and ex.side is not None and args.graph == -1:
-        # the graph candidate without the weight-gradient side stream (one stream: CIFAR
-        # ResNet-50 bs32 1.585 vs 1.785 ms; the side stream wins for larger steps)
-        side, ex.side = ex.side, None
-        sg1 = StepGraph(step, warmup=2)
-        m1, t1 = _pick({"graph": cands["graph"], "graph_one_stream": sg1.replay})
-        if m1 == "graph":
-            ex.side = side
-            del sg1
-        else:
-            cands["graph_one_stream"], mode = sg1.replay, m1
-        mode_times = {**(mode_times or {}), **t1}
+    if mode == "plan_one_stream":
+        plan = plan1
     run = cands[mode]
     use_graph = int(mode in ("graph", "graph_one_stream", "segmented"))
     # host enqueue time of the chosen mode: one step from an idle queue (nothing blocks), and
@@ -315,7 +320,7 @@ def main():
             "config": {"model": model, "global_batch": args.batch_size * world, "per_gpu_batch": args.batch_size,
                        "image_size": spec.image_size, "num_classes": spec.num_classes,
                        "parallelism": f"dp{world}", "hip_graph": bool(use_graph), "step_mode": mode,
-                       "wgrad_side_stream": ex.side is not None},
+                       "wgrad_side_stream": ex.side is not None and mode not in one_stream},
             "final_loss": round(loss, 4),
             "host_enqueue_ms": round(t_host, 3),
             "host_call_ms_median": round(sorted(t_calls)[len(t_calls) // 2] * 1e3, 3),

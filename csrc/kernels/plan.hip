@@ -58,6 +58,8 @@ struct Plan {
   std::vector<hipEvent_t> events;
   std::vector<hipStream_t> lanes;          // distinct streams, in order of first use
   std::vector<int> last_ev_entry;          // per event: its latest entry so far (recording)
+  std::vector<char> ev_waited;             // per event: some stream waits on it (else its records are dead)
+  size_t analyzed_n = 0;
   int launches = 0;
   int device = 0;
   // ---- multi-lane replay (drn_plan_set_threads) ----
@@ -126,8 +128,8 @@ static hipError_t issue(const Plan* p, const PlanEntry& x) {
       return x.func != nullptr ? hipModuleLaunchKernel(x.func, x.grid.x, x.grid.y, x.grid.z, x.block.x, x.block.y,
                                                        x.block.z, (unsigned)x.shm, x.stream, x.argv, nullptr)
                                : hipLaunchKernel(x.fn, x.grid, x.block, x.argv, x.shm, x.stream);
-    case PlanEntry::RECORD:
-      return hipEventRecord(p->events[x.ev], x.stream);
+    case PlanEntry::RECORD:  // (records nothing in the plan waits on -- most side-stream marks -- are skipped)
+      return p->ev_waited[x.ev] ? hipEventRecord(p->events[x.ev], x.stream) : hipSuccess;
     default:
       return hipStreamWaitEvent(x.stream, p->events[x.ev], 0);
   }
@@ -263,6 +265,23 @@ DRN_API int drn_plan_count(void* pv, int kind) {
   return n;
 }
 
+static void analyze(Plan* p) {
+  if (p->analyzed_n == p->e.size()) return;
+  p->ev_waited.assign(p->events.size(), 0);
+  for (const auto& x : p->e)
+    if (x.kind == PlanEntry::WAIT) p->ev_waited[x.ev] = 1;
+  p->analyzed_n = p->e.size();
+}
+
+// Event records replay actually issues (records of events no entry waits on are skipped).
+DRN_API int drn_plan_live_records(void* pv) {
+  Plan* p = static_cast<Plan*>(pv);
+  analyze(p);
+  int n = 0;
+  for (const auto& x : p->e) n += x.kind == PlanEntry::RECORD && p->ev_waited[x.ev];
+  return n;
+}
+
 static int replay_serial(Plan* p, int begin, int end) {
   for (int i = begin; i < end; ++i) {
     const hipError_t rc = drn::issue(p, p->e[i]);
@@ -275,6 +294,7 @@ static int replay_serial(Plan* p, int begin, int end) {
 DRN_API int drn_plan_replay(void* pv, int begin, int end) {
   Plan* p = static_cast<Plan*>(pv);
   if (begin < 0 || end > (int)p->e.size() || begin > end) return (int)hipErrorInvalidValue;
+  analyze(p);
   int nl = 0;
   for (int i = begin; i < end; ++i) nl = std::max(nl, p->e[i].lane + 1);
   bool null_stream = false;  // the legacy default stream orders against others by host order

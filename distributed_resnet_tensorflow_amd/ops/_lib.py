@@ -153,6 +153,7 @@ _SIGS = {
     "drn_plan_set_threads": ([c_p, c_int], c_int),
     "drn_plan_lanes": ([c_p], c_int),
     "drn_plan_count": ([c_p, c_int], c_int),
+    "drn_plan_live_records": ([c_p], c_int),
 }
 
 

@@ -166,6 +166,7 @@ class StepPlan:
     def stats(self) -> dict:
         L, p = self.L, self.p
         return {"launches": self.launches, "event_records": int(L.drn_plan_count(p, 1)),
+                "live_event_records": int(L.drn_plan_live_records(p)),
                 "stream_waits": int(L.drn_plan_count(p, 2)), "streams": int(L.drn_plan_lanes(p)),
                 "segments": sum(1 for _, a in self.cuts if a is not None) + 1, "threads": self.threads}
 

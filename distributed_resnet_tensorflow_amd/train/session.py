@@ -77,7 +77,8 @@ class TrainingSession:
     def __init__(self, spec, batch: int, cluster, *, weight_decay: float, lr_schedule, checkpoint_dir: str = "",
                  max_to_keep: int = 5, seed: int = 0, use_graph: bool = True, sync_mode: str = "sync",
                  bucket_mb: float = 25.0, meta: Optional[dict] = None, allreduce: str = "rccl", wire: str = "fp32",
-                 collective_timeout_s: float = 0.0, precision: str = "bf16", shard_optimizer: bool = False):
+                 collective_timeout_s: float = 0.0, precision: str = "bf16", shard_optimizer: bool = False,
+                 step_trial: bool = True):
         self.cluster = cluster
         self.spec = spec
         self.device = torch.device(cluster.device)
@@ -128,11 +129,18 @@ class TrainingSession:
         dp_ok = dp and self.engine.mode == "sync" and not self.sharded
         dp_graph = os.environ.get("DRN_DP_GRAPH", "auto")
         hip_cuda = self.device.type == "cuda" and self.be.name == "hip"
+        # (step_trial=False: a single-GPU session keeps the whole-step graph without timing it)
         self.use_graph = use_graph and hip_cuda and (
-            not dp or (dp_ok and self.engine.p2p is not None) or (dp_ok and dp_graph == "1"))
-        # step-mode trial of the RCCL data-parallel step: eager, native plan, segmented graphs
-        self._trial = {"modes": ["eager", "plan", "graph"], "i": 0, "n": 0, "t0": 0.0, "ms": {}} \
-            if (use_graph and hip_cuda and dp_ok and self.engine.p2p is None and dp_graph == "auto") else None
+            (dp_ok and self.engine.p2p is not None) or (dp_ok and dp_graph == "1") or (not dp and not step_trial))
+        # step-mode trial of the RCCL data-parallel step: eager, native plan, segmented graphs;
+        # of the single-GPU step: the whole-step graph (then its side-stream trial) or the native
+        # plan (ImageNet ResNet-50 bs128: plan 9.75 vs graph 10.52 ms, profiles/r5_bench_modes_v1.jsonl)
+        modes = None
+        if use_graph and hip_cuda and dp_ok and self.engine.p2p is None and dp_graph == "auto":
+            modes = ["eager", "plan", "graph"]
+        elif use_graph and hip_cuda and not dp and step_trial:
+            modes = ["graph", "plan"]
+        self._trial = {"modes": modes, "i": 0, "n": 0, "t0": 0.0, "ms": {}} if modes else None
         self._plan: Optional[StepPlan] = None
         self.graph_choice: Optional[dict] = None
         # single-GPU graph step: its first replays time the step with and without the weight-
@@ -141,7 +149,8 @@ class TrainingSession:
         self._strial = None
         # (also for the data-parallel P2P graph step: its reductions run on the P2P comm stream
         # either way, only the weight gradients move)
-        self._side_trial = (self.use_graph and (self.engine is None or self.engine.p2p is not None)
+        self._side_trial = ((self.use_graph or (self._trial is not None and self.engine is None))
+                            and (self.engine is None or self.engine.p2p is not None)
                             and self.ex.side is not None and os.environ.get("DRN_SIDE_TRIAL", "1") == "1")
         self.side_choice: Optional[dict] = None
         # graphs are captured and replayed from a NORMAL-priority stream (replay from the high-
@@ -294,12 +303,17 @@ class TrainingSession:
         W, K = self.TRIAL_WARM, self.TRIAL_STEPS
         if mode == "plan" and self._plan is None:
             torch.cuda.synchronize(self.device)
-            self._plan = StepPlan(self.ex, self.engine, 1.0 / self.world, warmup=1)
+            # (single GPU: one host thread per stream issues the replay)
+            self._plan = StepPlan(self.ex, self.engine, 1.0 / self.world, warmup=1,
+                                  threads=2 if (self.engine is None and self.ex.side is not None) else 1)
             return
         if mode == "graph" and self._graph is None:
             torch.cuda.synchronize(self.device)
-            self._graph = self._on_graph_stream(
-                lambda: SegmentedStepGraph(self.ex, self.engine, 1.0 / self.world, warmup=1))
+            if self.engine is None:
+                self._graph = self._on_graph_stream(lambda: StepGraph(self._step_body, warmup=1))
+            else:
+                self._graph = self._on_graph_stream(
+                    lambda: SegmentedStepGraph(self.ex, self.engine, 1.0 / self.world, warmup=1))
             return
         n = tr["n"]
         if n == W:
@@ -318,15 +332,19 @@ class TrainingSession:
         ms = agree_ms([tr["ms"][m] for m in modes], getattr(self.engine, "group", None))  # same mode everywhere
         pick = modes[min(range(len(modes)), key=lambda i: ms[i])]
         self.graph_choice = {f"{m}_ms": round(v, 3) for m, v in zip(modes, ms)}
-        self.graph_choice["mode"] = {"graph": "segmented graphs", "plan": "native plan"}.get(pick, "eager")
-        log.info("data-parallel step: %s -> %s", ", ".join(f"{m} {v:.3f} ms" for m, v in zip(modes, ms)),
-                 self.graph_choice["mode"])
+        graph_name = "segmented graphs" if self.engine is not None else "graph"
+        self.graph_choice["mode"] = {"graph": graph_name, "plan": "native plan"}.get(pick, "eager")
+        log.info("%s step: %s -> %s", "data-parallel" if self.engine is not None else "single-GPU",
+                 ", ".join(f"{m} {v:.3f} ms" for m, v in zip(modes, ms)), self.graph_choice["mode"])
         torch.cuda.synchronize(self.device)
         if pick != "graph":   # back to the eager structure: drop the graphs, weight gradients on the side stream
-            self.ex.side = self._graph.side_stream
+            self.ex.side = getattr(self._graph, "side_stream", self.ex.side)
             self._graph = None
         else:
             self.use_graph = True
+            if self._side_trial and self.engine is None:
+                # the whole-step graph: its side-stream trial follows (_side_trial_tick)
+                self._strial = ["side", 0, 0.0, 0.0, None, None, 0.0]
         if pick != "plan":
             self._plan = None
         self._mode = pick
@@ -337,6 +355,8 @@ class TrainingSession:
             self._step_body()
         elif mode == "plan":
             self._plan.replay()
+        elif self.engine is None:
+            self._on_graph_stream(self._graph.replay)
         else:
             self.engine.replay_begin()
             self._on_graph_stream(self._graph.replay)

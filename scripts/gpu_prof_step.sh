@@ -8,7 +8,7 @@ export PYTHONPATH=$ROOT
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/prof" -o step --output-format csv -- \
-  python3 "$ROOT/bench.py" --steps 5 --warmup 2 --graph 0 "$@" > "$ROOT/$OUT/prof.log" 2>&1 || { tail "$ROOT/$OUT/prof.log"; exit 1; }
+  python3 "$ROOT/bench.py" --steps 5 --warmup 2 --graph 0 --plan 0 "$@" > "$ROOT/$OUT/prof.log" 2>&1 || { tail "$ROOT/$OUT/prof.log"; exit 1; }
 cd "$ROOT"
 python3 scripts/prof_step.py "$OUT/prof/step_kernel_trace.csv" > "$OUT/step_summary.txt"
 python3 scripts/step_streams.py "$OUT/prof/step_kernel_trace.csv" > "$OUT/streams.txt" || true

@@ -12,7 +12,7 @@ i=0
 for ctrs in "SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE" \
             "FETCH_SIZE" "WRITE_SIZE"; do
   timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $ctrs -d "$OUT/p$i" -o pmc --output-format csv -- \
-    python3 "$ROOT/bench.py" --steps 2 --warmup 1 --graph 0 "$@" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; exit 1; }
+    python3 "$ROOT/bench.py" --steps 2 --warmup 1 --graph 0 --plan 0 "$@" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; exit 1; }
   i=$((i+1))
 done
 echo done

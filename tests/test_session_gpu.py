@@ -20,7 +20,7 @@ def test_graph_step_side_stream_trial(monkeypatch, trial):
     from distributed_resnet_tensorflow_amd.train.hooks import StopAtStepHook
     from distributed_resnet_tensorflow_amd.train.session import TrainingSession
     sess = TrainingSession(cifar_resnet_v2(8), 16, ClusterInfo(device="cuda:0"), weight_decay=2e-4,
-                           lr_schedule=lr_mod.for_dataset("cifar10"), use_graph=True)
+                           lr_schedule=lr_mod.for_dataset("cifar10"), use_graph=True, step_trial=False)
     assert sess.use_graph and sess.engine is None and sess.ex.side is not None
     sess.run(SyntheticFeeder(sess.ex, seed=0), [StopAtStepHook(50)])
     torch.cuda.synchronize()
@@ -85,7 +85,7 @@ def test_graph_step_staged_feeder_async_prefetch(tmp_path):
     ref = [np.array(next(ref_ld)[1], copy=True) for _ in range(steps)]
     ref_ld.close()
     sess = TrainingSession(cifar_resnet_v2(8), N, ClusterInfo(device="cuda:0"), weight_decay=2e-4,
-                           lr_schedule=lr_mod.for_dataset("cifar10"), use_graph=True)
+                           lr_schedule=lr_mod.for_dataset("cifar10"), use_graph=True, step_trial=False)
     captures = []
     hist = torch.empty(steps, N, dtype=torch.int32, device="cuda")
 
@@ -105,3 +105,30 @@ def test_graph_step_staged_feeder_async_prefetch(tmp_path):
     for k in range(steps):
         np.testing.assert_array_equal(hist[k].cpu().numpy(), ref[k], err_msg=f"labels of step {k}")
     assert float(sess.ex.metrics()["cross_entropy"]) == float(sess.ex.metrics()["cross_entropy"])
+
+
+def test_single_gpu_session_times_graph_and_plan():
+    """Single-GPU session (no engine): its first steps time the whole-step graph and the native
+    plan (runtime/plan.py, one host thread per stream) and keep the faster -- real training steps
+    throughout; a kept graph continues with its side-stream trial."""
+    from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2
+    from distributed_resnet_tensorflow_amd.parallel.cluster import ClusterInfo
+    from distributed_resnet_tensorflow_amd.train import lr as lr_mod
+    from distributed_resnet_tensorflow_amd.train.feeder import SyntheticFeeder
+    from distributed_resnet_tensorflow_amd.train.hooks import StopAtStepHook
+    from distributed_resnet_tensorflow_amd.train.session import TrainingSession
+    sess = TrainingSession(cifar_resnet_v2(8), 16, ClusterInfo(device="cuda:0"), weight_decay=2e-4,
+                           lr_schedule=lr_mod.for_dataset("cifar10"), use_graph=True)
+    assert not sess.use_graph and sess._trial is not None and sess.engine is None
+    sess.run(SyntheticFeeder(sess.ex, seed=0), [StopAtStepHook(40)])
+    torch.cuda.synchronize()
+    assert sess.global_step == 40 and sess.failed is None
+    c = sess.graph_choice
+    assert c is not None and c["graph_ms"] > 0 and c["plan_ms"] > 0, c
+    assert c["mode"] in ("graph", "native plan"), c
+    if c["mode"] == "graph":
+        assert sess.use_graph and sess._plan is None
+    else:
+        assert not sess.use_graph and sess._plan is not None and sess._plan.threads == 2
+    loss = float(sess.ex.metrics()["cross_entropy"])
+    assert loss == loss
