@@ -100,6 +100,7 @@ class BlockPlan:
 
 
 class Executor:
+    GRAD_BUF_MAX = 64     # rotating data-gradient buffers of ImageNet-sized steps (see _alloc)
     def __init__(self, spec: NetSpec, batch: int, backend, device, seed: int = 0,
                  weight_decay: float = 2e-4, momentum: float = 0.9, params: ParamStore | None = None,
                  materialize_bn: Optional[bool] = None):
@@ -454,8 +455,12 @@ class Executor:
         # buffers those waits cost ~1.5 ms of main-stream idle per ResNet-50 step). With the
         # critical path on the high-priority stream the side stream runs further behind: ResNet-50
         # bs128, one box, 3 rounds: 6 buffers 10.13-10.22 ms, 16: 10.07-10.13, 24: 10.01-10.05
-        # (profiles/r3s2_gradbufs.txt). Default 32 (~6.5 GB at ResNet-50 bs128), at most ~8 % of
-        # the device memory, for ImageNet-sized activations; small ones (CIFAR: latency-bound
+        # (profiles/r3s2_gradbufs.txt); 32 / 64 / 96: 9.771-9.804 / 9.762-9.780 / 9.755-9.778 ms
+        # (profiles/r5_grad_bufs_ab.txt: from 64 on the pool outnumbers the ~50 buffers a ResNet-50
+        # backward takes -- the LRU order restarts every step -- so no data gradient waits on a
+        # side-stream reader; 96 only adds unused buffers). Default 64 (~13 GB at ResNet-50 bs128
+        # of the 288 GB), at most ~8 % of the device memory, for ImageNet-sized activations; small
+        # ones (CIFAR: latency-bound
         # kernels on L2-resident tensors, 2.06-2.28 ms with 32 buffers vs 1.8-2.1 ms) keep 6.
         # Data parallelism uses the same pool: a bucket's all-reduce is issued from the side
         # stream right after the bucket's last weight gradient (_report), which is the earliest
@@ -466,7 +471,7 @@ class Executor:
         if self.side is not None and buf_bytes >= (64 << 20):
             cap = int(0.08 * torch.cuda.get_device_properties(self.device).total_memory) // max(1, buf_bytes) \
                 if self.device.type == "cuda" else 32
-            nbuf = max(6, min(32, cap))
+            nbuf = max(6, min(self.GRAD_BUF_MAX, cap))
         else:
             nbuf = 6 if self.side is not None else 3
         self.g_bufs = [self._act(max_act) for _ in range(nbuf)]
