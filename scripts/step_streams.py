@@ -68,3 +68,8 @@ print(f"main-stream gaps covered by other streams' kernels: {gap_cov / 1e3:.1f} 
       f"(truly idle GPU inside the step: {idle / 1e3:.1f} us)")
 print(f"main and other streams running concurrently: {both / 1e3:.1f} us "
       f"({both / max(1, sum(b - a for a, b in others)):.0%} of the other streams' busy time)")
+# the step's tail: the last kernels of both streams (start / end relative to the step end)
+print("tail (us before step end):")
+for r in step[-14:]:
+    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    print(f"  stream {r['Stream_Id']:>3} {(s - t1) / 1e3:8.1f} .. {(e - t1) / 1e3:8.1f}  {r['Kernel_Name'][:90]}")
