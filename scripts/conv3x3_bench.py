@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--json", default="")
+    ap.add_argument("--all", action="store_true", help="print every configuration's time")
     a = ap.parse_args()
     be = HipBackend()
     be.autotune = False
@@ -59,6 +60,8 @@ def main():
                 if be.L.drn_conv_fwd2(ctypes.byref(args), be.zero_page.data_ptr(), be.stream()) != 0:
                     continue
                 t = timeit(lambda: be.launch_conv(args), a.iters)
+                if a.all:
+                    print(f"   {H:2d}x{H:<2d} {name:5s} cfg {cfg:3d} {t:7.1f} us", flush=True)
                 best = min(best, (t, cfg))
             t, cfg = best
             print(f"{H:2d}x{H:<2d} {C:3d}->{C:3d} {name:5s} best cfg {cfg:3d} {t:7.1f} us {flop / t / 1e6:6.0f} TF/s",

@@ -48,14 +48,18 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--json", default="")
+    ap.add_argument("--variants", default="", help="comma-separated subset of the variant names")
+    ap.add_argument("--layers", default="", help="comma-separated layer indices of LAYERS")
     a = ap.parse_args()
     be = HipBackend()
     be.autotune = False
     cfgs = [100] + list(range(be.L.drn_conv_glds_num_cfgs()))
     out = []
     N = a.batch
-    for H, C, K, k, s in LAYERS:
+    for li, (H, C, K, k, s) in enumerate(LAYERS):
         if a.only and a.only != f"{k}x{k}":
+            continue
+        if a.layers and str(li) not in a.layers.split(","):
             continue
         P = (H + 2 * (k // 2) - k) // s + 1
         x = torch.randn(N, H, H, C, device="cuda").bfloat16()
@@ -75,8 +79,12 @@ def main():
             ("pro+stats", dict(in_bn=(sc, sh), stats=st), xb + yb),
             ("pro+res+stats", dict(in_bn=(sc, sh), residual=res, stats=st), xb + 2 * yb),
             ("bnbwd", dict(stats=st, bn_bwd=(bx, v[0], v[1], v[2], v[3])), xb + 2 * yb),
+            ("stats_rep1", dict(stats=torch.zeros(1, 2, K, device="cuda")), xb + yb),
+            ("stats_rep64", dict(stats=torch.zeros(64, 2, K, device="cuda")), xb + yb),
         )
         for name, kw, nbytes in variants:
+            if a.variants and name not in a.variants.split(","):
+                continue
             best = (float("inf"), None)
             for cfg in cfgs:
                 args = be.conv_args(x, w, y, g, **kw)
