@@ -14,7 +14,7 @@ import pytest
 import torch
 
 from distributed_resnet_tensorflow_amd.models.spec import build_spec
-from distributed_resnet_tensorflow_amd.ops.backend import ConvGeom, HipBackend, OutMap, RefBackend
+from distributed_resnet_tensorflow_amd.ops.backend import BnCfin, ConvGeom, HipBackend, OutMap, RefBackend
 from distributed_resnet_tensorflow_amd.runtime.executor import Executor
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not torch.cuda.is_available(), reason="no GPU")]
@@ -105,6 +105,19 @@ def test_bench_geometry_conv(key):
     om = OutMap(P, Q, a0.out_stride, a0.out_oh, a0.out_ow) if mapped else None
     g = ConvGeom(a0.stride, a0.pad_h, a0.pad_w, a0.dil)
     in_bn = (torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.3) if a0.in_scale else None
+    fin = None
+    G = keys[i][-1]  # the recorded launch finalized its input BN in the prologue from G replicas
+    if G:
+        # replica sums of a known per-channel mean / variance (all in replica 0); the reference
+        # applies the scale / shift they finalize to
+        n = float(N * H * W)
+        mu, var = torch.randn(C, device=dev) * 0.3, torch.rand(C, device=dev) + 0.5
+        gamma, beta = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.3
+        stats = torch.zeros(G, 2, C, device=dev)
+        stats[0, 0], stats[0, 1] = mu * n, (var + mu * mu) * n
+        fin = BnCfin(stats, n, gamma, beta=beta, publish=False)
+        sc = gamma / torch.sqrt(var + fin.eps)
+        in_bn = (sc, beta - mu * sc)
     res = torch.randn(N, oH, oW, K, device=dev).bfloat16() if a0.residual else None
     bb = None
     if a0.bn_x:
@@ -116,7 +129,7 @@ def test_bench_geometry_conv(key):
     if res is not None and mapped:
         y.copy_(res)            # accumulating phase launch: residual == output
         res = y
-    a = be.conv_args(x, w, y, g, in_bn=in_bn, residual=res, stats=st, out_map=om, bn_bwd=bb)
+    a = be.conv_args(x, w, y, g, in_bn=in_bn, residual=res, stats=st, out_map=om, bn_bwd=bb, in_fin=fin)
     assert be.conv_key(a) == keys[i]
     cfg = be.conv_cfg.get(keys[i])
     assert cfg is not None, "the benchmark launch was not tuned"
