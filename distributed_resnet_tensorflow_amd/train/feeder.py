@@ -57,12 +57,21 @@ class _StagedFeeder:
     session calls AFTER it has enqueued step k, so the host reads and decodes while the GPU
     computes. The H2D copies of batch k+1 wait only for the preprocess of batch k (an event), not
     for the whole step. A caller that never calls `prefetch()` gets it at the next `next()`.
+
+    COPY_STREAM: whether the H2D copies get a stream of their own. Off for CIFAR (a batch is
+    ~100 KB, a few microseconds of copy): the copies go on the consuming stream instead. A fifth
+    busy stream in the process (beside the critical-path, weight-gradient, report and RCCL
+    streams) shares one of the GPU_MAX_HW_QUEUES=4 hardware queues with a compute stream, and the
+    cross-stream waits then serialise them: the CIFAR ResNet-50 bs32 CLI over RCCL ran 9.15 ms per
+    step with the copy stream vs 2.05 ms without it, single-GPU 1.92 vs 1.81 ms
+    (profiles/r5_cli_step_rate.txt). On for ImageNet, whose tens of MB per batch must overlap.
     """
+    COPY_STREAM = True
 
     def _init_staging(self, ex):
         self.ex = ex
         self.gpu = ex.device.type == "cuda"
-        self.copy_stream = torch.cuda.Stream(device=ex.device) if self.gpu else None
+        self.copy_stream = torch.cuda.Stream(device=ex.device) if self.gpu and self.COPY_STREAM else None
         self._pending = None
         self._consumed = None          # event after the preprocess of the batch last handed out
         self._main = None              # the stream that consumes the batches (set by next())
@@ -72,8 +81,16 @@ class _StagedFeeder:
         self._exhausted = False
 
     def _stage(self, pairs):
-        """pairs: [(device dst, host src)]; enqueues the copies on the copy stream."""
+        """pairs: [(device dst, host src)]; enqueues the copies on the copy stream (or, without
+        one, on the consuming stream: stream order after the previous batch's preprocess and
+        before the next one's; prefetch may run on a worker thread, hence the explicit stream)."""
         if self.gpu:
+            if self.copy_stream is None:
+                with torch.cuda.stream(self._main or torch.cuda.current_stream(self.ex.device)):
+                    for dst, src in pairs:
+                        dst.copy_(_as_tensor(src), non_blocking=True)
+                self._pending = None
+                return
             # the device staging buffers are free once the previous batch's preprocess has read them
             if self._consumed is not None:
                 self.copy_stream.wait_event(self._consumed)
@@ -133,6 +150,8 @@ class _StagedFeeder:
 
 
 class CifarFeeder(_StagedFeeder):
+    COPY_STREAM = False
+
     def __init__(self, ex, loader: "cifar_data.CifarLoader", is_training: bool):
         self.loader, self.train = loader, is_training
         N, dev = ex.N, ex.device

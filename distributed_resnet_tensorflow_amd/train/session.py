@@ -139,9 +139,12 @@ class TrainingSession:
         if use_graph and hip_cuda and dp_ok and self.engine.p2p is None and dp_graph == "auto":
             modes = ["eager", "plan", "graph"]
         elif use_graph and hip_cuda and not dp and step_trial:
-            modes = ["graph", "plan"]
+            # (+ the plan recorded without the weight-gradient side stream: small steps, e.g. CIFAR
+            # ResNet-50 bs32: bench 1.59 ms one-stream vs 1.70 ms two-stream plan)
+            modes = ["graph", "plan"] + (["plan_one_stream"] if self.ex.side is not None else [])
         self._trial = {"modes": modes, "i": 0, "n": 0, "t0": 0.0, "ms": {}} if modes else None
         self._plan: Optional[StepPlan] = None
+        self._plan1: Optional[StepPlan] = None     # (trial candidate: one-stream plan)
         self.graph_choice: Optional[dict] = None
         # single-GPU graph step: its first replays time the step with and without the weight-
         # gradient side stream and keep the faster (CIFAR ResNet-50 bs32: one stream 1.585 ms vs
@@ -307,6 +310,14 @@ class TrainingSession:
             self._plan = StepPlan(self.ex, self.engine, 1.0 / self.world, warmup=1,
                                   threads=2 if (self.engine is None and self.ex.side is not None) else 1)
             return
+        if mode == "plan_one_stream" and self._plan1 is None:
+            torch.cuda.synchronize(self.device)
+            side, self.ex.side = self.ex.side, None
+            try:
+                self._plan1 = StepPlan(self.ex, None, warmup=1)
+            finally:
+                self.ex.side = side
+            return
         if mode == "graph" and self._graph is None:
             torch.cuda.synchronize(self.device)
             if self.engine is None:
@@ -333,7 +344,8 @@ class TrainingSession:
         pick = modes[min(range(len(modes)), key=lambda i: ms[i])]
         self.graph_choice = {f"{m}_ms": round(v, 3) for m, v in zip(modes, ms)}
         graph_name = "segmented graphs" if self.engine is not None else "graph"
-        self.graph_choice["mode"] = {"graph": graph_name, "plan": "native plan"}.get(pick, "eager")
+        self.graph_choice["mode"] = {"graph": graph_name, "plan": "native plan",
+                                     "plan_one_stream": "native plan (one stream)"}.get(pick, "eager")
         log.info("%s step: %s -> %s", "data-parallel" if self.engine is not None else "single-GPU",
                  ", ".join(f"{m} {v:.3f} ms" for m, v in zip(modes, ms)), self.graph_choice["mode"])
         torch.cuda.synchronize(self.device)
@@ -345,8 +357,12 @@ class TrainingSession:
             if self._side_trial and self.engine is None:
                 # the whole-step graph: its side-stream trial follows (_side_trial_tick)
                 self._strial = ["side", 0, 0.0, 0.0, None, None, 0.0]
-        if pick != "plan":
+        if pick == "plan_one_stream":
+            # the step stays on one stream from here on (eager fallbacks included)
+            self._plan, self.ex.side = self._plan1, None
+        elif pick != "plan":
             self._plan = None
+        self._plan1 = None
         self._mode = pick
         self._trial = None
 
@@ -355,6 +371,8 @@ class TrainingSession:
             self._step_body()
         elif mode == "plan":
             self._plan.replay()
+        elif mode == "plan_one_stream":
+            self._plan1.replay()
         elif self.engine is None:
             self._on_graph_stream(self._graph.replay)
         else:

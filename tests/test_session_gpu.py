@@ -108,9 +108,10 @@ def test_graph_step_staged_feeder_async_prefetch(tmp_path):
 
 
 def test_single_gpu_session_times_graph_and_plan():
-    """Single-GPU session (no engine): its first steps time the whole-step graph and the native
-    plan (runtime/plan.py, one host thread per stream) and keep the faster -- real training steps
-    throughout; a kept graph continues with its side-stream trial."""
+    """Single-GPU session (no engine): its first steps time the whole-step graph, the native
+    plan (runtime/plan.py, one host thread per stream) and the plan recorded on one stream, and
+    keep the fastest -- real training steps throughout; a kept graph continues with its
+    side-stream trial."""
     from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2
     from distributed_resnet_tensorflow_amd.parallel.cluster import ClusterInfo
     from distributed_resnet_tensorflow_amd.train import lr as lr_mod
@@ -120,15 +121,18 @@ def test_single_gpu_session_times_graph_and_plan():
     sess = TrainingSession(cifar_resnet_v2(8), 16, ClusterInfo(device="cuda:0"), weight_decay=2e-4,
                            lr_schedule=lr_mod.for_dataset("cifar10"), use_graph=True)
     assert not sess.use_graph and sess._trial is not None and sess.engine is None
-    sess.run(SyntheticFeeder(sess.ex, seed=0), [StopAtStepHook(40)])
+    sess.run(SyntheticFeeder(sess.ex, seed=0), [StopAtStepHook(60)])  # (trial: 3 x 14 steps)
     torch.cuda.synchronize()
-    assert sess.global_step == 40 and sess.failed is None
+    assert sess.global_step == 60 and sess.failed is None
     c = sess.graph_choice
     assert c is not None and c["graph_ms"] > 0 and c["plan_ms"] > 0, c
-    assert c["mode"] in ("graph", "native plan"), c
+    assert c["plan_one_stream_ms"] > 0, c
+    assert c["mode"] in ("graph", "native plan", "native plan (one stream)"), c
     if c["mode"] == "graph":
         assert sess.use_graph and sess._plan is None
-    else:
+    elif c["mode"] == "native plan":
         assert not sess.use_graph and sess._plan is not None and sess._plan.threads == 2
+    else:
+        assert not sess.use_graph and sess._plan is not None and sess.ex.side is None
     loss = float(sess.ex.metrics()["cross_entropy"])
     assert loss == loss
