@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--resnet_size", type=int, default=50)
     ap.add_argument("--width", type=int, default=1, help="bottleneck width multiplier (2 = Wide-ResNet-50-2)")
     ap.add_argument("--batch_size", type=int, default=128, help="per-GPU batch")
+    ap.add_argument("--image_size", type=int, default=224,
+                    help="ImageNet input size (rehearsals of the ResNet-50 topology at a small shape; not the headline)")
     ap.add_argument("--graph", type=int, default=-1, help="capture the step in a HIP graph (-1: auto)")
     ap.add_argument("--plan", type=int, default=-1,
                     help="native step plan (runtime/plan.py): -1 auto (timed against the other modes), 0 off, 1 force")
@@ -80,6 +82,9 @@ def main():
                           RANK="0", WORLD_SIZE="1")
     from distributed_resnet_tensorflow_amd.models.spec import build_spec
     spec = build_spec(args.dataset, args.resnet_size, width=args.width)
+    if args.dataset == "imagenet" and args.image_size != 224:
+        from distributed_resnet_tensorflow_amd.models.spec import imagenet_resnet_v2
+        spec = imagenet_resnet_v2(args.resnet_size, width=args.width, image_size=args.image_size)
     # the P2P all-reduce (chosen by --allreduce p2p, or auto for <= 64 MB of gradients) runs the
     # data-parallel step as one HIP graph; RCCL data parallelism runs it eagerly
     from distributed_resnet_tensorflow_amd.parallel.engine import p2p_wanted
@@ -283,6 +288,15 @@ def main():
     ms = dt / args.steps * 1e3
     img_s = args.batch_size * world * args.steps / dt
     loss = float(ex.loss_vec.float().mean())
+    in_sync = None
+    if world > 1:
+        # after the timed region: every replica must hold bit-identical weights (an exact integer
+        # checksum of the fp32 masters, gathered from every rank)
+        ck = ex.P.master.view(torch.int32).to(torch.int64).sum().reshape(1)
+        ck = ck if backend == "nccl" else ck.cpu()
+        allck = [torch.zeros_like(ck) for _ in range(world)]
+        dist.all_gather(allck, ck)
+        in_sync = all(bool(torch.equal(allck[0], c)) for c in allck)
     dp = None
     if eng is not None:
         # data-parallel diagnostics of the last timed step (rank 0's view; comm_exposed_ms = the
@@ -295,15 +309,22 @@ def main():
         for k in ("backward_ms", "comm_exposed_ms", "comm_ms", "overlap_fraction"):
             if k in st:
                 dp[k] = round(float(st[k]), 3)
+        if in_sync is not None:
+            dp["replicas_in_sync"] = in_sync
+        if plan is not None and mode.startswith("plan"):
+            # native segments between the engine's Python-issued bucket collectives
+            dp["plan_report_cuts"] = sum(1 for _, act in plan.cuts if isinstance(act, tuple))
     if rank == 0:
-        base = BASELINE_IMG_S.get(args.dataset, {}).get(world) if (args.width == 1 and args.resnet_size == 50) else None
+        base = BASELINE_IMG_S.get(args.dataset, {}).get(world) \
+            if (args.width == 1 and args.resnet_size == 50 and spec.image_size in (224, 32)) else None
         model = f"resnet{args.resnet_size}_v2_{args.dataset}" if args.dataset == "imagenet" else \
             f"cifar10_resnet{args.resnet_size}_v2"
         if args.width > 1:
             model = f"wide_resnet{args.resnet_size}_{args.width}_{args.dataset}"
         out = {
             "metric": "images/sec (whole node) ResNet-50 bs=128/GPU"
-            if (args.dataset == "imagenet" and args.resnet_size == 50 and args.width == 1 and args.batch_size == 128)
+            if (args.dataset == "imagenet" and args.resnet_size == 50 and args.width == 1 and args.batch_size == 128
+                and spec.image_size == 224)
             else f"images/sec (whole node) {model} bs={args.batch_size}/GPU",
             "value": round(img_s, 2),
             "unit": "images/sec",

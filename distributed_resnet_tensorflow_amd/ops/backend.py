@@ -360,6 +360,9 @@ class HipBackend(_Common):
             if need > self.ks_ws.numel():
                 if torch.cuda.is_current_stream_capturing():
                     raise RuntimeError("split-K workspace must be sized before graph capture (autotune first)")
+                # a recorded native plan / captured graph keeps the raw pointer of the old buffer:
+                # it stays referenced (never freed under a live plan), the growth is monotone
+                HipBackend._retired_ws.append(self.ks_ws)
                 self.ks_ws = torch.empty(need, dtype=torch.float32, device=self.device)
             a.ks_ws, a.ks_tickets = self.ks_ws.data_ptr(), self.ks_tickets.data_ptr()
 
@@ -796,6 +799,10 @@ class HipBackend(_Common):
                                           1 if relu else 0, self.stream()), "drn_bnrelu_pool")
 
     _sgemm_ws: dict = {}
+    # superseded split-K / sgemm workspaces: native step plans and HIP graphs replay raw device
+    # pointers, so a workspace a plan may have recorded is never returned to the allocator
+    # (growth is monotone, so this at most doubles the workspace footprint)
+    _retired_ws: list = []
     SGEMM_TARGET_WG = 256
 
     def sgemm(self, ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, bias=None):
@@ -809,6 +816,10 @@ class HipBackend(_Common):
             key = (C.device, self.stream())
             ws = HipBackend._sgemm_ws.get(key)
             if ws is None or ws.numel() < need:
+                if ws is not None:
+                    if torch.cuda.is_current_stream_capturing():
+                        raise RuntimeError("sgemm workspace must be sized before graph capture")
+                    HipBackend._retired_ws.append(ws)  # (plans recorded earlier keep its pointer)
                 ws = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=C.device)
                 HipBackend._sgemm_ws[key] = ws
         _lib.check(self.L.drn_sgemm(int(ta), int(tb), M, N, K, float(alpha), A.data_ptr(), lda, B.data_ptr(), ldb,

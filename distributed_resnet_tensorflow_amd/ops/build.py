@@ -91,20 +91,16 @@ def _stamp_object() -> Path:
     return obj
 
 
-def _headers_mtime() -> float:
-    hs = list(INCLUDE.glob("*.h"))
-    return max((h.stat().st_mtime for h in hs), default=0.0)
-
-
-def _compile(src: Path, extra: list[str], obj_dir: Optional[Path] = None) -> Path:
+def _compile(src: Path, extra: list[str], obj_dir: Optional[Path] = None, include: Path = INCLUDE) -> Path:
     obj = (obj_dir or OBJ_DIR) / (src.stem + ".o")
-    if obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, _headers_mtime()):
+    hdr = max((h.stat().st_mtime for h in include.glob("*.h")), default=0.0)
+    if obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, hdr):
         return obj
     # DRN_CONV_TRACE=1: diagnostics build with the per-workgroup conv timeline
     # (scripts/trace_conv.py); never the default -- the instrumentation costs ~2.5 % of a step
     trace = ["-DDRN_CONV_TRACE"] if os.environ.get("DRN_CONV_TRACE") == "1" else []
     trace += os.environ.get("DRN_HIPCC_EXTRA", "").split()  # A/B builds (e.g. -DDRN_KORDER_TAP_OUTER)
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-I", str(INCLUDE),
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-I", str(include),
            "-Wno-unused-result", "-c", str(src), "-o", str(obj)] + trace + extra
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
@@ -178,17 +174,21 @@ def build(force: bool = False, verbose: bool = True, extra: list[str] | None = N
     return LIB_PATH
 
 
-def build_variant(out_dir: str, extra: list[str]) -> Path:
+def build_variant(out_dir: str, extra: list[str], src_root: Optional[str] = None) -> Path:
     """A diagnostics / A-B variant of the kernel library (e.g. extra=["-DDRN_CONV_TRACE"]) built
     into out_dir/libdrn_kernels.so with its own objects; load it with DRN_KERNEL_LIB=<path>
-    (the source-stamp check is skipped for an explicit library)."""
+    (the source-stamp check is skipped for an explicit library). src_root: a directory holding
+    kernels/ and include/ to build instead of csrc/ (patched copies for experiments, e.g.
+    scripts/conv_bound_iso.py)."""
     out = Path(out_dir).resolve()
-    obj_dir = REPO / "build" / ("variant_" + out.name)  # objects stay out of the shipped tree
+    obj_dir = REPO / "build" / ("variant_" + out.parent.name + "_" + out.name)  # objects stay out of the tree
     out.mkdir(parents=True, exist_ok=True)
     obj_dir.mkdir(parents=True, exist_ok=True)
-    srcs = sources()
+    kdir = Path(src_root) / "kernels" if src_root else KERNELS
+    inc = Path(src_root) / "include" if src_root else INCLUDE
+    srcs = sorted(kdir.glob("*.hip"))
     with cf.ThreadPoolExecutor(max_workers=min(len(srcs), 8)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, list(extra), obj_dir), srcs))
+        objs = list(ex.map(lambda s: _compile(s, list(extra), obj_dir, inc), srcs))
     objs.append(_stamp_object())
     lib = out / "libdrn_kernels.so"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(lib)] + [str(o) for o in objs]

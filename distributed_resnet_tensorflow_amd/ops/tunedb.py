@@ -19,7 +19,9 @@ Two files, as MIOpen keeps a system and a user database:
     scripts/make_tune_db.py) and is only ever READ: no run, test or bench rewrites it;
   * the USER database ``DRN_TUNE_DB`` (default ``~/.cache/drn/tune_db.json``) receives every
     choice this process timed itself; it is consulted for geometries the system database lacks.
-``DRN_TUNE_DB=off`` disables both. Writes are read-merge-write through a temporary file and
+``DRN_TUNE_DB=off`` disables both; ``DRN_TUNE_DB_SYSTEM=off`` disables only the system database
+(scripts/make_tune_db.py rebuilds the shipped file that way, so every geometry is re-timed and
+the output holds the complete section, not just what the shipped file lacked). Writes are read-merge-write through a temporary file and
 ``os.replace`` (several ranks of one node may write concurrently; the last rename wins, every
 version is a complete file). Sections of other library hashes are dropped when a section is
 written (they can never match again).
@@ -39,6 +41,10 @@ _LOCK = threading.Lock()
 
 def enabled() -> bool:
     return os.environ.get("DRN_TUNE_DB", "").lower() not in ("off", "0", "none")
+
+
+def system_enabled() -> bool:
+    return enabled() and os.environ.get("DRN_TUNE_DB_SYSTEM", "").lower() not in ("off", "0", "none")
 
 
 def db_path() -> Optional[Path]:
@@ -71,7 +77,7 @@ class TuneDB:
     def __init__(self, section: str, path: Optional[Path] = None, system: Optional[Path] = None):
         self.section = section
         self.path = db_path() if path is None else path
-        on = enabled() or path is not None
+        on = system_enabled() or (path is not None and system is not None)
         self.sys_conv, self.sys_wgrad = _load_section(SYSTEM_PATH if system is None else system, section) if on \
             else ({}, {})
         self.conv, self.wgrad = _load_section(self.path, section)  # this process's / the user's choices

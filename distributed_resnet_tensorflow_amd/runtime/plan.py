@@ -130,6 +130,7 @@ class StepPlan:
         if engine is not None:
             ex.grad_ready = lambda lo: None   # (reports become plan cuts: PlanSched.cut)
         _lib.check(self.L.drn_plan_record_begin(self.p), "drn_plan_record_begin")
+        ok = False
         try:
             ex.forward(train=True)
             if engine is None:
@@ -141,20 +142,33 @@ class StepPlan:
                 self._cut("finish")
                 self._grad = engine.wire_buf if engine.wire_buf is not None else ex.P.grad
                 ex.apply_gradients(grad_scale=grad_scale, grad=self._grad)
+            ok = True
         finally:
             self.L.drn_plan_record_end()
             ex.sched, be.recording = old, False
             ex.grad_ready = None
+            if not ok:
+                # a failed recording leaves plan events in the executor's carry-over state: the
+                # next eager step would hand them to torch's stream API
+                self._clear_carry()
         self._cut(None)
         if sched.recorded_keys != sched.waited_keys:
             raise RuntimeError(f"plan carry-in events unbalanced: recorded {sched.recorded_keys}, "
                                f"waited {sched.waited_keys} (record the plan after an eager step)")
         # the recorded step's events are plan events: an eager step after replays must not wait on
-        # them through torch (mixing eager steps and replays needs a device synchronize)
-        ex._tflip_ev = ex._tail_ev = ex._stem_ev = None
+        # them through torch; replay() leaves a torch event for the side-stream weight refresh
+        self._clear_carry()
+        self._tflip = "tflip" in sched.recorded_keys
+        self._tflip_torch = None
         self.launches = int(self.L.drn_plan_launches(self.p))
         self.set_threads(threads)
         torch.cuda.synchronize()
+
+    def _clear_carry(self):
+        ex = self.ex
+        ex._tflip_ev = ex._tail_ev = ex._stem_ev = None
+        ex._marks.clear()
+        ex._pending.clear()
 
     def set_threads(self, n: int):
         """Host threads issuing a replay: 1 = the calling thread, in recorded order; n > 1 = one
@@ -202,6 +216,14 @@ class StepPlan:
                 ex._report(action[1])
         if eng is None:
             ex._tail_ev = None          # (the recorded step joined its deferred tail itself)
+        if self._tflip and ex.side is not None:
+            # the replay ended with the data-gradient weight refresh on the side stream: an eager
+            # backward after it waits for that refresh (a torch event after the side stream's
+            # replayed work, as the eager step's own "tflip" event would be)
+            if self._tflip_torch is None:
+                self._tflip_torch = torch.cuda.Event()
+            self._tflip_torch.record(ex.side)
+            ex._tflip_ev = self._tflip_torch
 
     def close(self):
         if self.p is not None:

@@ -68,7 +68,7 @@ class _LazyGraph:
 
     def replay(self):
         if self.g is None:
-            self.g = StepGraph(self.sess._step_body, warmup=1)
+            self.g = self.sess._on_graph_stream(lambda: StepGraph(self.sess._step_body, warmup=1))
         else:
             self.g.replay()
 
@@ -161,8 +161,14 @@ class TrainingSession:
         # the eager step moves to the high-priority stream below, the segmented-graph candidate of
         # the trial keeps this one
         self._graph_stream = None
+        if hip_cuda and (self.use_graph or (modes is not None and "graph" in modes)):
+            # whole-step / segmented graphs are captured and replayed from a dedicated normal-
+            # priority stream of their own, not from the stream current at init (the process's
+            # null stream in the CLI, which the feeder's batch copies and preprocessing queue
+            # behind: single-GPU graph trial 5.5-7.2 ms there vs 1.68 ms in bench.py,
+            # profiles/r5_cli_step_rate.txt)
+            self._graph_stream = torch.cuda.Stream(self.device)
         if not self.use_graph and self.device.type == "cuda" and self.be.name == "hip":
-            self._graph_stream = torch.cuda.current_stream(self.device)
             # eager step (data parallel or not): the critical path on its own high-priority HW
             # queue, ahead of the weight-gradient side stream (ResNet-50 bs128 on one GPU: 9.93 vs
             # 10.17 ms per step, profiles/r3_side_stream_ab.txt)
@@ -263,7 +269,7 @@ class TrainingSession:
                     self._graph = self._on_graph_stream(
                         lambda: SegmentedStepGraph(self.ex, self.engine, 1.0 / self.world, warmup=1))
                 else:
-                    self._graph = StepGraph(self._step_body, warmup=1)
+                    self._graph = self._on_graph_stream(lambda: StepGraph(self._step_body, warmup=1))
                     if self._side_trial:
                         # [phase, replays in phase, t0, side ms, (side graph, side stream),
                         #  one-stream graph, one-stream ms]

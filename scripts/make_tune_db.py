@@ -10,6 +10,8 @@ by the library's source hash: rebuild it whenever a kernel source changes).
 import os
 import sys
 
+# every geometry re-timed: the shipped (system) database is not consulted while rebuilding it
+os.environ["DRN_TUNE_DB_SYSTEM"] = "off"
 os.environ.setdefault("DRN_TUNE_ITERS", "20")
 os.environ.setdefault("DRN_TUNE_TOP", "4")        # (more finalists made the in-situ pick noisier)
 os.environ.setdefault("DRN_INSITU_ROUNDS", "3")

@@ -189,6 +189,106 @@ def test_bench_multirank_code_path_one_device():
     assert r["n_gpus"] == 2 and r["config"]["global_batch"] == 256 and r["value"] > 0
 
 
+def _bench_two_ranks(args):
+    env = dict(os.environ, DRN_BENCH_BACKEND="gloo", DRN_BENCH_ONE_DEVICE="1", PYTHONPATH=REPO)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(REPO, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1"] + args
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    import json
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(420)
+@pytest.mark.parametrize("net", ["cifar20", "imagenet50_64px"])
+def test_bench_multirank_rccl_plan_path_one_device(net):
+    """the production N>1 ResNet path -- bucket collectives issued from Python
+    between the segments of a native step plan (--allreduce rccl --plan 1, what bench.py picks for
+    ResNet-50 at N>1) -- run by bench.py under torchrun at world 2 (gloo transport, both ranks on
+    cuda:0). Both replicas must end bit-identical, and the plan must be cut at the bucket reports.
+    imagenet50_64px: the ImageNet ResNet-50 topology (stem, maxpool, 4 stages, 1001 classes) at
+    64x64 inputs."""
+    if net == "cifar20":
+        args = ["--dataset", "cifar10", "--resnet_size", "20", "--bucket_mb", "0.05"]
+    else:
+        args = ["--dataset", "imagenet", "--resnet_size", "50", "--image_size", "64", "--batch_size", "8",
+                "--bucket_mb", "4"]
+    r = _bench_two_ranks(args + ["--allreduce", "rccl", "--plan", "1"])
+    dp = r["data_parallel"]
+    assert r["n_gpus"] == 2 and dp["rccl_world"] == 2 and dp["allreduce"] == "rccl", r
+    assert r["config"]["step_mode"].startswith("plan"), r["config"]
+    assert dp["replicas_in_sync"] is True, dp
+    assert dp["plan_report_cuts"] >= 2 and dp["buckets"] >= 2, dp
+    assert r["value"] > 0 and r["final_loss"] == r["final_loss"]
+
+
+def _plan_dp_worker(rank, world, port, q, threads):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DRN_DETERMINISTIC="1")
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2
+        from distributed_resnet_tensorflow_amd.ops.backend import HipBackend
+        from distributed_resnet_tensorflow_amd.parallel.engine import DataParallelEngine
+        from distributed_resnet_tensorflow_amd.runtime.plan import StepPlan
+        spec, N = cifar_resnet_v2(8), 8
+        be = HipBackend("cuda")                 # one backend: identical kernel configurations
+        states, cuts = [], 0
+        for mode in ("eager", "plan"):
+            ex = _make(spec, N, rank, seed=1 + rank, be=be)
+            ex.set_lr(0.1)
+            eng = DataParallelEngine(ex, bucket_mb=0.05, allreduce="rccl")
+            assert eng.p2p is None and len(eng.buckets) > 2
+            eng.broadcast_parameters()
+            if mode == "eager":
+                for _ in range(4):
+                    ex.forward(True)
+                    eng.begin_step()
+                    ex.backward()
+                    eng.apply_gradients(eng.finish(), 1.0 / world)
+            else:
+                plan = StepPlan(ex, eng, grad_scale=1.0 / world, warmup=1, threads=threads)
+                cuts = sum(1 for _, a in plan.cuts if isinstance(a, tuple))
+                for _ in range(3):
+                    plan.replay()
+            torch.cuda.synchronize()
+            states.append([t.clone() for t in (ex.P.master, ex.P.momentum, ex.P.bn_state, ex.P.wbf16)])
+        bitwise = all(torch.equal(x, y) for x, y in zip(*states))
+        ck = states[1][0].view(torch.int32).to(torch.int64).sum().reshape(1).cpu()
+        gathered = [torch.zeros_like(ck) for _ in range(world)]
+        dist.all_gather(gathered, ck)
+        same = all(torch.equal(gathered[0], t) for t in gathered)
+        q.put((rank, bitwise, same, cuts))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), False, 0))
+
+
+@pytest.mark.parametrize("threads", [1, 2])
+def test_plan_replay_data_parallel_two_ranks_bitwise(threads):
+    """tests/test_plan_gpu.py's data-parallel plan test at world 2: on each of two ranks (gloo,
+    one GPU), 1 eager step + 3 native plan replays with the bucket all-reduces between the plan
+    segments end bitwise equal to 4 eager data-parallel steps, and both ranks hold the same
+    weights (deterministic mode)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_plan_dp_worker, args=(r, 2, port, q, threads)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, bitwise, same, cuts in res:
+        assert bitwise is True, (rank, bitwise)
+        assert same and cuts >= 2, (rank, same, cuts)
+
+
 def _graph_p2p_worker(rank, world, port, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DRN_DETERMINISTIC="1")

@@ -147,3 +147,61 @@ def test_plan_replay_data_parallel_bitwise(monkeypatch, threads):
             assert torch.equal(x, y), name
     finally:
         dist.destroy_process_group()
+
+
+def test_plan_replay_survives_workspace_growth(monkeypatch):
+    """a plan replays the raw pointers of the backend's split-K and sgemm workspaces.
+    Growing them after the recording (another executor with larger GEMMs / split-K convs in the
+    same process) must not free the recorded buffers: the replays stay bitwise equal to eager
+    steps even with the allocator's free memory overwritten by NaNs in between."""
+    monkeypatch.setenv("DRN_DETERMINISTIC", "1")
+    from distributed_resnet_tensorflow_amd.models.spec import imagenet_resnet_v2
+    from distributed_resnet_tensorflow_amd.ops.backend import ConvGeom, HipBackend
+    from distributed_resnet_tensorflow_amd.runtime.executor import Executor
+    from distributed_resnet_tensorflow_amd.runtime.plan import StepPlan
+
+    be = HipBackend("cuda")            # one backend: identical tuned kernel configurations
+
+    def make():
+        ex = Executor(imagenet_resnet_v2(50, num_classes=11, image_size=64), 4, be, "cuda", seed=5,
+                      weight_decay=1e-4)
+        be.synthetic_images(ex.images, seed=9)
+        ex.labels.copy_(torch.arange(4, dtype=torch.int32))
+        ex.set_lr(0.02)
+        return ex
+
+    a = make()
+    for _ in range(4):
+        _eager_step(a)
+    want = _state(a)
+    b = make()
+    plan = StepPlan(b, warmup=1)
+    key = (b.P.master.device, be.stream())
+    old_sgemm = HipBackend._sgemm_ws.get(key)
+    assert old_sgemm is not None, "the ImageNet head's split-K sgemm must use the workspace"
+    old_ks = be.ks_ws
+    # grow both workspaces: a big fp32 GEMM on the same stream, a split-K conv
+    # (64 x 64 output, K = 32768: split-K over 256 workgroups; a wide ldc sizes the partials)
+    A = torch.randn(64, 32768, device="cuda")
+    B = torch.randn(32768, 64, device="cuda")
+    C = torch.empty(64, 4096, device="cuda")
+    be.sgemm(False, False, 64, 64, 32768, 1.0, A, 32768, B, 64, 0.0, C, 4096)
+    x = torch.randn(64, 28, 28, 128, device="cuda").bfloat16()
+    w = (torch.randn(128, 3, 3, 128, device="cuda") * 0.05).bfloat16()
+    y = torch.empty(64, 28, 28, 128, device="cuda", dtype=torch.bfloat16)
+    g = ConvGeom(1, 1, 1)
+    be.conv_cfg[be.conv_key(be.conv_args(x, w, y, g))] = (0, 4)
+    be.launch_conv(be.conv_args(x, w, y, g))
+    torch.cuda.synchronize()
+    assert HipBackend._sgemm_ws[key] is not old_sgemm and be.ks_ws is not old_ks
+    assert any(t is old_sgemm for t in HipBackend._retired_ws) and any(t is old_ks for t in HipBackend._retired_ws)
+    del A, B, C, x, w, y
+    # whatever the allocator holds free is overwritten: a freed recorded workspace would show
+    free = (torch.cuda.memory_reserved() - torch.cuda.memory_allocated()) // 4 // 2
+    junk = torch.full((max(int(free), 1),), float("nan"), device="cuda")
+    for _ in range(3):
+        plan.replay()
+    got = _state(b)
+    del junk
+    for name, x_, y_ in zip(("master", "momentum", "bn_state", "wbf16"), got, want):
+        assert torch.equal(x_, y_), name

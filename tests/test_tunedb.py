@@ -112,3 +112,21 @@ def test_system_database_is_read_only_and_read_first(tmp_path, monkeypatch):
     w = TuneDB("gfx950/256cu|abcd")         # pointed at the system file: writes are refused
     w.put_conv((8,), (1, 1))
     assert not w.save() and sysdb.read_text() == before
+
+
+def test_system_database_can_be_switched_off(tmp_path, monkeypatch):
+    """DRN_TUNE_DB_SYSTEM=off (scripts/make_tune_db.py, gpu_make_db.sh): a rebuild re-times every
+    geometry instead of taking the shipped choices, so its output is a complete section."""
+    from distributed_resnet_tensorflow_amd.ops import tunedb
+    sysdb, user = tmp_path / "system.json", tmp_path / "user.json"
+    s = TuneDB("gfx950/256cu|abcd", sysdb)
+    s.put_conv((1, 2), (7, 1))
+    assert s.save()
+    monkeypatch.setattr(tunedb, "SYSTEM_PATH", sysdb)
+    monkeypatch.setenv("DRN_TUNE_DB", str(user))
+    assert TuneDB("gfx950/256cu|abcd").get_conv((1, 2)) == (7, 1)
+    monkeypatch.setenv("DRN_TUNE_DB_SYSTEM", "off")
+    db = TuneDB("gfx950/256cu|abcd")
+    assert db.get_conv((1, 2)) is None
+    db.put_conv((1, 2), (3, 1))
+    assert db.save() and json.loads(user.read_text())["sections"]["gfx950/256cu|abcd"]["conv"]["1,2"] == [3, 1]
