@@ -62,6 +62,7 @@ def main():
     result_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
 
+    import distributed_resnet_tensorflow_amd  # noqa: F401 -- its HIP queue default (GPU_MAX_HW_QUEUES) precedes HIP init
     import torch
     import torch.distributed as dist
 
@@ -341,7 +342,8 @@ def main():
             "config": {"model": model, "global_batch": args.batch_size * world, "per_gpu_batch": args.batch_size,
                        "image_size": spec.image_size, "num_classes": spec.num_classes,
                        "parallelism": f"dp{world}", "hip_graph": bool(use_graph), "step_mode": mode,
-                       "wgrad_side_stream": ex.side is not None and mode not in one_stream},
+                       "wgrad_side_stream": ex.side is not None and mode not in one_stream,
+                       "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")},
             "final_loss": round(loss, 4),
             "host_enqueue_ms": round(t_host, 3),
             "host_call_ms_median": round(sorted(t_calls)[len(t_calls) // 2] * 1e3, 3),

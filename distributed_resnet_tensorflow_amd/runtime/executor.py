@@ -99,6 +99,27 @@ class BlockPlan:
     grad_lo: int                    # lowest flat grad offset written by this block
 
 
+_CU_STREAMS: dict = {}
+
+
+def _side_stream(backend, device):
+    """The weight-gradient side stream: a plain normal-priority stream, or with DRN_SIDE_CUS=n a
+    stream whose kernels may use only n of the device's CUs (csrc/kernels/plan.hip
+    drn_stream_create_cu_mask), so the critical-path data gradients never wait for CUs held by
+    weight gradients. One such stream per (device, n) for the process lifetime."""
+    n = int(os.environ.get("DRN_SIDE_CUS", "0") or 0)
+    if n <= 0:
+        return torch.cuda.Stream(device)
+    key = (str(device), n)
+    if key not in _CU_STREAMS:
+        total = torch.cuda.get_device_properties(device).multi_processor_count
+        ptr = backend.L.drn_stream_create_cu_mask(min(n, total), total)
+        if not ptr:
+            raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({n} of {total} CUs)")
+        _CU_STREAMS[key] = torch.cuda.ExternalStream(ptr, device=device)
+    return _CU_STREAMS[key]
+
+
 class Executor:
     GRAD_BUF_MAX = 64     # rotating data-gradient buffers of ImageNet-sized steps (see _alloc)
     def __init__(self, spec: NetSpec, batch: int, backend, device, seed: int = 0,
@@ -153,7 +174,7 @@ class Executor:
         # gradient-buffer claims skip the cross-queue wait when the reader already finished
         self.claim_query = True
         if self.is_hip and os.environ.get("DRN_WGRAD_STREAM", "1") == "1":
-            self.side = torch.cuda.Stream(self.device)
+            self.side = _side_stream(backend, self.device)
         # gradient-buffer reuse guard: id(buffer) -> sequence number of the side-stream weight
         # gradient that last read it; _marks[seq] = event recorded after that weight gradient;
         # the main stream has waited for the side stream up to _synced

@@ -64,7 +64,11 @@ class _StagedFeeder:
     streams) shares one of the GPU_MAX_HW_QUEUES=4 hardware queues with a compute stream, and the
     cross-stream waits then serialise them: the CIFAR ResNet-50 bs32 CLI over RCCL ran 9.15 ms per
     step with the copy stream vs 2.05 ms without it, single-GPU 1.92 vs 1.81 ms
-    (profiles/r5_cli_step_rate.txt). On for ImageNet, whose tens of MB per batch must overlap.
+    (profiles/r5_cli_step_rate.txt). On for ImageNet, whose tens of MB per batch must overlap; the
+    hardware-queue sharing itself is gone since the package sets GPU_MAX_HW_QUEUES=8 (one queue
+    per stream): the ImageNet data-parallel step with this copy stream 10.0-10.1 ms vs 15.0-15.2 ms
+    with 4 queues, and 11.5 ms with the copies on the consuming stream
+    (profiles/r6_imagenet_copy_stream.jsonl).
     """
     COPY_STREAM = True
 
@@ -204,7 +208,8 @@ class ImagenetFeeder(_StagedFeeder):
             else:
                 torch.cuda.synchronize(self.ex.device)
             self.d_buf = torch.empty(int(n * 1.25), dtype=torch.uint8, device=self.ex.device)
-            self.d_buf.record_stream(self.copy_stream)
+            if self.copy_stream is not None:
+                self.d_buf.record_stream(self.copy_stream)
             if self._main is not None:
                 self.d_buf.record_stream(self._main)
         self._stage([(self.d_buf[:n], packed), (self.d_desc, desc_bytes), (self.d_lab, labels)])
