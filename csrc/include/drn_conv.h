@@ -206,11 +206,4 @@ struct DrnConvWgradArgs {
   // 1: every split adds its tile into out = the final, pre-zeroed gradient with fp32 atomics
   // (no partial slabs, no drn_splitk_reduce)
   int32_t atomic_out;
-  // non-null (splits > 1, LDS-DMA pipelines): in-kernel split-K reduction -- every split stores
-  // its partial slab into out, takes a ticket on red_tickets[tile] (zero before the launch; the
-  // last arriver re-arms it), and the LAST arriver of a tile sums the tile's slabs in split order
-  // into red_out (the final gradient, overwritten): no drn_splitk_reduce launch
-  float* red_out;
-  uint32_t* red_tickets;  // >= DRN_WGRAD_TICKETS words
 };
-#define DRN_WGRAD_TICKETS 65536

@@ -91,51 +91,6 @@ __device__ __forceinline__ void wgrad_store(const DrnConvWgradArgs& a, f32x4_t (
     }
 }
 
-// In-kernel split-K reduction (DrnConvWgradArgs::red_out): the split's slab is already stored;
-// the guide's last-arriver hand-off (cdna_hip_programming.md §5 "Projection GEMM" item 2, G16):
-// every storing wave drains its stores, the workgroup barrier, ONE agent-scope release by lane 0
-// before its relaxed ticket add; the workgroup drawing the last ticket acquires (agent scope)
-// and sums the tile's slabs in split order 0..splits-1 (fixed: bitwise reproducible whatever the
-// arrival order; its own split comes from its registers, bit-identical to its stored slab) and
-// writes the final gradient. Nobody waits on anybody: no deadlock at any residency. The tile's
-// splits run on one XCD under the remap above, so the slab reads are mostly L2 hits.
-template <int MI, int MJ>
-__device__ __forceinline__ void wgrad_fused_reduce(const DrnConvWgradArgs& a, f32x4_t (&acc)[MI][MJ], int split,
-                                                   int tile, int cb, int kb, int Ktot, int lane, char* smem) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int* flag = reinterpret_cast<int*>(smem);  // (the one dynamic LDS array: no second __shared__ object)
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(a.red_tickets + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t + 1u == (unsigned)a.splits;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(a.red_tickets + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  if (!*flag) return;
-  const size_t slab = (size_t)a.K * Ktot;
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < MJ; ++j) {
-      const int co = cb + 16 * j + (lane & 15);
-      const int kr = kb + 16 * i + 4 * (lane >> 4);
-      if (co < a.K && kr < Ktot) {
-        const float* p = a.out + (size_t)co * Ktot + kr;
-        f32x4_t sum = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        for (int s = 0; s < a.splits; ++s)
-          sum += s == split ? acc[i][j] : *reinterpret_cast<const f32x4_t*>(p + (size_t)s * slab);
-        *reinterpret_cast<f32x4_t*>(a.red_out + (size_t)co * Ktot + kr) = sum;
-      }
-    }
-}
-
 template <int BKK, int BCO, bool PRO, int NST>
 __global__ __launch_bounds__(256, NST == 1 ? 4 : 2) void conv_wgrad_kernel(DrnConvWgradArgs a) {
   constexpr int BP = 64;                 // pixels per step
@@ -739,7 +694,6 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
   if (trace != nullptr) t_loop = wg_realtime();
 #endif
   wgrad_store<MI, MJ>(a, acc, split, c0 + wc * WCO, k0 + wk * WKK, Ktot, lane);
-  if (a.red_out != nullptr) wgrad_fused_reduce<MI, MJ>(a, acc, split, tile, c0 + wc * WCO, k0 + wk * WKK, Ktot, lane, smem);
 #ifdef DRN_CONV_TRACE
   if (trace != nullptr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -913,8 +867,8 @@ DRN_API int drn_wgrad_tiles(int Ktot, int K) {
 }
 
 DRN_API int drn_conv_wgrad(DrnConvWgradArgs* a, hipStream_t s) {
-  if ((a->C % 8) != 0 || (a->K % 8) != 0 || a->splits < 1 || (a->pix_per_split % 64) != 0 || a->red_out != nullptr)
-    return (int)hipErrorInvalidValue;  // (the register-staged kernel has no in-kernel reduction)
+  if ((a->C % 8) != 0 || (a->K % 8) != 0 || a->splits < 1 || (a->pix_per_split % 64) != 0)
+    return (int)hipErrorInvalidValue;
   return a->in_scale != nullptr ? drn::dispatch_wgrad<true>(a, s) : drn::dispatch_wgrad<false>(a, s);
 }
 
@@ -925,12 +879,6 @@ DRN_API int drn_conv_wgrad2(DrnConvWgradArgs* a, const void* zero, int ns, hipSt
   const bool packed = a->C == 4 && a->S % 2 == 0 && a->in_scale == nullptr && zero != nullptr && ns != 0;
   if (((a->C % 8) != 0 && !packed) || (a->K % 8) != 0 || a->splits < 1 || (a->pix_per_split % 64) != 0)
     return (int)hipErrorInvalidValue;
-  if (a->red_out != nullptr) {  // in-kernel split-K reduction: split slabs + tickets, LDS-DMA pipelines
-    const int Ktot = a->R * a->S * a->C;
-    if (a->splits < 2 || a->atomic_out || a->red_tickets == nullptr || zero == nullptr || ns == 0 ||
-        drn_wgrad_tiles(Ktot, a->K) > DRN_WGRAD_TICKETS)
-      return (int)hipErrorInvalidValue;
-  }
   // (the LDS-DMA kernels' fused BN prologue always applies the ReLU: pre-activation v2)
   if (zero == nullptr || ns == 0 || (a->in_scale != nullptr && a->relu_in == 0)) return drn_conv_wgrad(a, s);
   return drn::dispatch_wgrad_glds(a, zero, ns, s);

@@ -325,21 +325,3 @@ DRN_API int drn_plan_replay(void* pv, int begin, int end) {
   }
   return p->err.load();
 }
-
-// A stream whose kernels may run only on `ncu` of the device's `total` compute units (mask bits
-// evenly spaced over the CU index, so every XCD keeps some): the weight-gradient side stream under
-// DRN_SIDE_CUS, so the critical-path stream's next data gradient always finds CUs the side stream's
-// weight gradients cannot hold. nullptr on failure.
-DRN_API void* drn_stream_create_cu_mask(int ncu, int total) {
-  if (total <= 0 || total > 1024 || ncu <= 0 || ncu > total) return nullptr;
-  std::vector<uint32_t> mask((total + 31) / 32, 0u);
-  for (int k = 0; k < ncu; ++k) {
-    const int cu = (int)((long)k * total / ncu);
-    mask[cu / 32] |= 1u << (cu % 32);
-  }
-  hipStream_t s = nullptr;
-  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) return nullptr;
-  return s;
-}
-
-DRN_API int drn_stream_destroy(void* s) { return (int)hipStreamDestroy(static_cast<hipStream_t>(s)); }

@@ -73,7 +73,7 @@ class DrnConvWgradArgs(ctypes.Structure):
         ("N", c_int), ("H", c_int), ("W", c_int), ("C", c_int), ("K", c_int), ("R", c_int), ("S", c_int),
         ("P", c_int), ("Q", c_int), ("stride", c_int), ("pad_h", c_int), ("pad_w", c_int), ("relu_in", c_int),
         ("splits", c_int), ("pix_per_split", c_int), ("fd_pq", DrnFastDiv), ("fd_q", DrnFastDiv),
-        ("atomic_out", c_int), ("red_out", c_p), ("red_tickets", c_p),
+        ("atomic_out", c_int),
     ]
 
 
@@ -150,8 +150,6 @@ _SIGS = {
     "drn_plan_size": ([c_p], c_int),
     "drn_plan_launches": ([c_p], c_int),
     "drn_plan_replay": ([c_p, c_int, c_int], c_int),
-    "drn_stream_create_cu_mask": ([c_int, c_int], c_p),
-    "drn_stream_destroy": ([c_p], c_int),
     "drn_plan_set_threads": ([c_p, c_int], c_int),
     "drn_plan_lanes": ([c_p], c_int),
     "drn_plan_count": ([c_p, c_int], c_int),

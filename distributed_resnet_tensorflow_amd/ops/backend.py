@@ -243,9 +243,6 @@ class HipBackend(_Common):
         # wgrad_atomic_used when some layer picked it
         self.wgrad_atomic_ok = False
         self.wgrad_atomic_used = False
-        # in-kernel split-K reduction of the weight gradients (output mode 2): one ticket word per
-        # weight-gradient tile, zero between launches (the last arriver of a tile re-arms it)
-        self.wgrad_tickets = torch.zeros(65536, dtype=torch.int32, device=self.device)  # DRN_WGRAD_TICKETS
         self.forced_wgrad_ns = None  # a fixed weight-gradient pipeline (tests / experiments)
         self.tune_log: list = []
         self._db = None   # persistent kernel-selection database (ops/tunedb.py), loaded on first use
@@ -551,15 +548,8 @@ class HipBackend(_Common):
     # 32: 32 steps) otherwise get 4 splits, i.e. 20-64 workgroups walking 8 serial steps each
     WGRAD_MIN_STEPS_CANDS = (8, 2)
 
-    # weight-gradient output modes (tuner / database field 2): fp32 partial slabs + a separate
-    # deterministic reduce launch; fp32 atomics into the zeroed gradient; slabs + in-kernel
-    # last-arriver reduction (csrc/kernels/conv_wgrad.hip wgrad_fused_reduce)
-    WG_SLAB, WG_ATOMIC, WG_FUSED = 0, 1, 2
-
     def wgrad_args(self, x, dy, out, g: ConvGeom, in_bn=None, relu_in=True, ws=None, target_blocks: int = 0,
-                   atomic=False, min_steps: int = 0):
-        """atomic: the output mode (False/0 slabs, True/1 fp32 atomics, 2 in-kernel reduction)."""
-        mode = int(atomic)
+                   atomic: bool = False, min_steps: int = 0):
         N, H, W, C = x.shape
         N2, P, Q, K = dy.shape
         Kd, R, S, Cd = out.shape
@@ -576,15 +566,13 @@ class HipBackend(_Common):
         a.splits, a.pix_per_split = splits, pps
         a.fd_pq = _lib.DrnFastDiv.make(P * Q)
         a.fd_q = _lib.DrnFastDiv.make(Q)
-        if splits == 1 or mode == self.WG_ATOMIC:
+        if splits == 1 or atomic:
             a.out = out.data_ptr()
-            a.atomic_out = 1 if (mode == self.WG_ATOMIC and splits > 1) else 0
+            a.atomic_out = 1 if (atomic and splits > 1) else 0
         else:
             need = splits * out.numel()
             assert ws is not None and ws.numel() >= need, f"wgrad workspace too small ({need})"
             a.out = ws.data_ptr()
-            if mode == self.WG_FUSED:
-                a.red_out, a.red_tickets = out.data_ptr(), self.wgrad_tickets.data_ptr()
         a._keep = (x, dy, out, in_bn, ws)  # (raw pointers above: keep the tensors alive)
         return a
 
@@ -602,18 +590,12 @@ class HipBackend(_Common):
     def wgrad_key(a) -> tuple:
         return (a.N, a.H, a.W, a.C, a.K, a.R, a.S, a.P, a.Q, a.stride, a.pad_h, a.pad_w, a.in_scale is not None)
 
-    def _wgrad_modes(self) -> tuple:
-        """Output modes the weight-gradient tuner may choose (DRN_WGRAD_MODES restricts them for
-        A/B runs; a database choice outside the set is re-tuned)."""
-        env = os.environ.get("DRN_WGRAD_MODES")
-        return tuple(int(m) for m in env.split(",")) if env else (self.WG_SLAB, self.WG_ATOMIC, self.WG_FUSED)
-
     def _wgrad_kernel(self, a, ns: int, st):
         _lib.check(self.L.drn_conv_wgrad2(ctypes.byref(a), self.zero_page.data_ptr(), ns, st), "drn_conv_wgrad")
 
     def _wgrad_full(self, a, ns: int, out, st):
         self._wgrad_kernel(a, ns, st)
-        if a.splits > 1 and not a.atomic_out and not a.red_out:
+        if a.splits > 1 and not a.atomic_out:
             _lib.check(self.L.drn_splitk_reduce(a.out, out.data_ptr(), out.numel(), a.splits, 1.0, 0, st),
                        "drn_splitk_reduce")
 
@@ -626,7 +608,7 @@ class HipBackend(_Common):
         st = self.stream()
         cands = tuple(int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6,7,8").split(","))
         seen = set()
-        modes = tuple(m for m in self._wgrad_modes() if m != self.WG_ATOMIC or self.wgrad_atomic_ok)
+        modes = (False, True) if self.wgrad_atomic_ok else (False,)
 
         def time_one(a, ns, n):
             return self._timed(lambda: self._wgrad_full(a, ns, out, st), n)
@@ -635,18 +617,17 @@ class HipBackend(_Common):
         for tgt, atomic, ms_min in [(t, m, k) for t in self.WGRAD_TARGETS for m in modes
                                     for k in self.WGRAD_MIN_STEPS_CANDS]:
             a = args_for(tgt, atomic, ms_min)
-            eff = atomic if a.splits > 1 else self.WG_SLAB
-            if (a.splits, eff) in seen:
+            if (a.splits, a.atomic_out) in seen:
                 continue
-            seen.add((a.splits, eff))
+            seen.add((a.splits, a.atomic_out))
             for ns in cands:
                 if self.L.drn_conv_wgrad2(ctypes.byref(a), self.zero_page.data_ptr(), ns, st) != 0:
                     continue  # pipeline not available for this launch
                 for _ in range(2):
                     self._wgrad_full(a, ns, out, st)
-                first.append((time_one(a, ns, iters), (tgt, ns, int(eff), ms_min), a))
+                first.append((time_one(a, ns, iters), (tgt, ns, bool(a.atomic_out), ms_min), a))
         if not first:
-            return (0, 2, self.WG_SLAB, 0)
+            return (0, 2, False, 0)
         # pass 2 (as the forward tuner): the 4 fastest re-timed twice, interleaved, each keeping its
         # best -- single 5-launch timings of ~10-us CIFAR kernels picked outliers (run-to-run step
         # spread 1.77-1.95 ms at batch 32)
@@ -656,7 +637,7 @@ class HipBackend(_Common):
             for r in top:
                 r[0] = min(r[0], time_one(r[2], r[1][1], 2 * iters))
         best_t, best, _ = min(top, key=lambda r: r[0])
-        if best[2] == self.WG_ATOMIC:
+        if best[2]:
             self.wgrad_atomic_used = True  # the executor now zeroes the gradients every step
         self.tune_log.append((("wgrad",) + key, best, round(best_t * 1e3, 1)))
         return best
@@ -674,18 +655,17 @@ class HipBackend(_Common):
         if key not in self.wgrad_ns and self.autotune and not torch.cuda.is_current_stream_capturing():
             hit = self.tune_db().get_wgrad(key)
             cands = [int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6,7,8").split(",")]
-            if hit is not None and (hit[2] != self.WG_ATOMIC or self.wgrad_atomic_ok) and hit[1] in cands \
-                    and hit[2] in self._wgrad_modes():
+            if hit is not None and (not hit[2] or self.wgrad_atomic_ok) and hit[1] in cands:
                 self.db_hits += 1
                 self.wgrad_ns[key] = hit
-                if hit[2] == self.WG_ATOMIC:
+                if hit[2]:
                     self.wgrad_atomic_used = True  # the executor now zeroes the gradients every step
             else:
                 self.wgrad_ns[key] = self._tune_wgrad(args_for, out, key)
                 self.tune_db().put_wgrad(key, self.wgrad_ns[key])
-            if self.wgrad_ns[key][2] == self.WG_ATOMIC:
+            if self.wgrad_ns[key][2]:
                 self.zero_(out)  # the timing launches left partial sums in this gradient slot
-        tgt, ns, atomic, ms = self.wgrad_ns.get(key, (0, 2, self.WG_SLAB, 0))
+        tgt, ns, atomic, ms = self.wgrad_ns.get(key, (0, 2, False, 0))
         if tgt or atomic or ms:
             a = args_for(tgt, atomic, ms)
         self._wgrad_full(a, ns, out, st)

@@ -93,15 +93,14 @@ class TuneDB:
         self.conv[_key(key)] = [int(val[0]), int(val[1])]
         self.dirty = True
 
-    # wgrad: (split target, pipeline, output mode (0 slabs + reduce, 1 atomics, 2 in-kernel
-    # reduction; older files hold a bool: False / True = 0 / 1), min steps)
+    # wgrad: (split target, pipeline, atomic, min steps)
     def get_wgrad(self, key) -> Optional[tuple]:
         k = _key(key)
         v = self.sys_wgrad.get(k, self.wgrad.get(k))
-        return (int(v[0]), int(v[1]), int(v[2]), int(v[3])) if v is not None else None
+        return (int(v[0]), int(v[1]), bool(v[2]), int(v[3])) if v is not None else None
 
     def put_wgrad(self, key, val) -> None:
-        self.wgrad[_key(key)] = [int(val[0]), int(val[1]), int(val[2]), int(val[3])]
+        self.wgrad[_key(key)] = [int(val[0]), int(val[1]), bool(val[2]), int(val[3])]
         self.dirty = True
 
     def save(self) -> bool:

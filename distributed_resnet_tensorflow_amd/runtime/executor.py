@@ -99,27 +99,6 @@ class BlockPlan:
     grad_lo: int                    # lowest flat grad offset written by this block
 
 
-_CU_STREAMS: dict = {}
-
-
-def _side_stream(backend, device):
-    """The weight-gradient side stream: a plain normal-priority stream, or with DRN_SIDE_CUS=n a
-    stream whose kernels may use only n of the device's CUs (csrc/kernels/plan.hip
-    drn_stream_create_cu_mask), so the critical-path data gradients never wait for CUs held by
-    weight gradients. One such stream per (device, n) for the process lifetime."""
-    n = int(os.environ.get("DRN_SIDE_CUS", "0") or 0)
-    if n <= 0:
-        return torch.cuda.Stream(device)
-    key = (str(device), n)
-    if key not in _CU_STREAMS:
-        total = torch.cuda.get_device_properties(device).multi_processor_count
-        ptr = backend.L.drn_stream_create_cu_mask(min(n, total), total)
-        if not ptr:
-            raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({n} of {total} CUs)")
-        _CU_STREAMS[key] = torch.cuda.ExternalStream(ptr, device=device)
-    return _CU_STREAMS[key]
-
-
 class Executor:
     GRAD_BUF_MAX = 64     # rotating data-gradient buffers of ImageNet-sized steps (see _alloc)
     def __init__(self, spec: NetSpec, batch: int, backend, device, seed: int = 0,
@@ -165,8 +144,9 @@ class Executor:
         # BN-backward chain of the critical path; events guard the gradient buffers it reads.
         # Only weight gradients (conv_wgrad, its own workspace) run there: the split-K conv
         # workspace and tickets of the backend are used by main-stream launches alone.
-        # (Forking the projection-shortcut forward conv onto this stream measured neutral, and a
-        # CU-masked side stream +0-0.4 %; both were removed.)
+        # (Forking the projection-shortcut forward conv onto this stream measured neutral; a
+        # CU-masked side stream (hipExtStreamCreateWithCUMask) 5 % slower at 64, 128 and 192 of
+        # 256 CUs, profiles/r6_experiments.md; both were removed.)
         self.side = None
         # the data-gradient weight refresh after each update on the side stream (eager steps;
         # neutral vs the main stream, profiles/r4_tflip_side_ab.txt)
@@ -174,7 +154,7 @@ class Executor:
         # gradient-buffer claims skip the cross-queue wait when the reader already finished
         self.claim_query = True
         if self.is_hip and os.environ.get("DRN_WGRAD_STREAM", "1") == "1":
-            self.side = _side_stream(backend, self.device)
+            self.side = torch.cuda.Stream(self.device)
         # gradient-buffer reuse guard: id(buffer) -> sequence number of the side-stream weight
         # gradient that last read it; _marks[seq] = event recorded after that weight gradient;
         # the main stream has waited for the side stream up to _synced

@@ -5,11 +5,11 @@ mkdir -p gpurun_out/r6
 OUT=gpurun_out/r6/ab7.jsonl
 : > $OUT
 for round in 1 2; do
-  for arm in base hwq4 nofused cu128 cu192 cu64; do
+  for arm in base hwq4 fusedonly cu128 cu192 cu64; do
     case $arm in
       base) env="" ;;
       hwq4) env="GPU_MAX_HW_QUEUES=4" ;;
-      nofused) env="DRN_WGRAD_MODES=0,1" ;;
+      fusedonly) env="DRN_WGRAD_MODES=2" ;;
       cu128) env="DRN_SIDE_CUS=128" ;;
       cu192) env="DRN_SIDE_CUS=192" ;;
       cu64) env="DRN_SIDE_CUS=64" ;;

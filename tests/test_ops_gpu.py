@@ -974,43 +974,6 @@ def test_wgrad_atomic_split_k(hip, ref, case, ns):
     assert rel(dw, dw_ref) < 1e-2
 
 
-@pytest.mark.parametrize("case", [(4, 16, 16, 16, 3, 1, 1), (4, 24, 64, 32, 1, 1, 0), (4, 33, 32, 64, 3, 2, 1),
-                                  (8, 14, 256, 256, 3, 1, 1), (16, 7, 512, 128, 1, 1, 0)])
-@pytest.mark.parametrize("ns", [2, 3, 5, 7])
-def test_wgrad_fused_split_k_reduction(hip, ref, case, ns):
-    """Split-K weight gradient with the in-kernel last-arriver reduction (output mode 2): the split
-    slabs are summed by the last workgroup of each tile into the gradient (no reduce launch,
-    every stale value overwritten), equal to the fp32 reference; bitwise equal to itself on a
-    re-run (fixed split order), the tickets re-armed for the next launch; the register-staged
-    pipeline refuses the mode."""
-    N, H, C, K, R, s, p = case
-    torch.manual_seed(37 + ns)
-    P = (H + 2 * p - R) // s + 1
-    x = bf(torch.randn(N, H, H, C))
-    dy = bf(torch.randn(N, P, P, K))
-    g = ConvGeom(s, p, p)
-    dw_ref = torch.zeros(K, R, R, C)
-    ref.conv_wgrad(x.float(), dy.float(), dw_ref, g)
-    ws = torch.zeros(max(1, hip.wgrad_ws_elems(N * P * P, K, R, R, C)), device="cuda")
-    dw = torch.full((K, R, R, C), float("nan"), device="cuda")
-    xd, dyd = x.cuda(), dy.cuda()   # (the launch arguments hold raw pointers: keep the tensors alive)
-    a = hip.wgrad_args(xd, dyd, dw, g, ws=ws, target_blocks=4096, min_steps=2, atomic=hip.WG_FUSED)
-    assert a.splits > 1 and a.atomic_out == 0 and a.red_out
-    assert hip.L.drn_conv_wgrad2(ctypes.byref(a), hip.zero_page.data_ptr(), 0, hip.stream()) != 0
-    if K <= 32 and ns in (4, 5, 6):  # narrow 32-channel dY tiles: 64-pixel stages only
-        assert hip.L.drn_conv_wgrad2(ctypes.byref(a), hip.zero_page.data_ptr(), ns, hip.stream()) != 0
-        return
-    hip._wgrad_full(a, ns, dw, hip.stream())
-    torch.cuda.synchronize()
-    assert rel(dw, dw_ref) < 1e-2
-    first = dw.clone()
-    dw.fill_(float("nan"))
-    hip._wgrad_full(a, ns, dw, hip.stream())
-    torch.cuda.synchronize()
-    assert torch.equal(dw, first)
-    assert int(hip.wgrad_tickets.abs().sum()) == 0
-
-
 @pytest.mark.parametrize("N,H", [(2, 16), (3, 30), (2, 224)])
 def test_packed_stem(hip, ref, N, H):
     """Packed stem (csrc/kernels/stem.hip): the 7x7/2 conv over a 4-channel, column-padded copy of
