@@ -48,6 +48,10 @@ CASES = {
     "wgrad3x3_28": ("wgrad", 128, 28, 128, 128, 3, 1, 1, dict(ns=2, target=512)),
     "wgrad3x3_14": ("wgrad", 128, 14, 256, 256, 3, 1, 1, dict(ns=2, target=512)),
     "wgrad1x1_14": ("wgrad", 128, 14, 1024, 256, 1, 1, 0, dict(ns=2, target=512)),
+    # the packed 7x7/2 stem's weight gradient (4-channel tap-pair layout, csrc/kernels/stem.hip):
+    # input [N][224][226][4], taps 7 x 8 (the 8th tap zero), pad (3, 2); the last kernel of the step
+    "fwd_stem": ("fwd", 128, 224, 4, 64, 7, 2, 3, dict(cfg=12, S=8, W=226, pad_w=2)),
+    "wgrad_stem": ("wgrad", 128, 224, 4, 64, 7, 2, 3, dict(ns=2, target=512, S=8, W=226, pad_w=2)),
 }
 # --sweep: the 3x3 forward shapes under other tile / pipeline configurations (name@cfg)
 SWEEP = {"fwd3x3_28": (1, 2, 8, 9, 17, 20, 27, 30, 31), "fwd3x3_14": (1, 2, 8, 9, 17, 20, 25, 26, 29, 30)}
@@ -86,12 +90,13 @@ def run(only=None, iters=50):
     for name, (kind, N, H, C, K, R, stride, pad, ex) in CASES.items():
         if only and name not in only:
             continue
+        S, W, pad_w = ex.get("S", R), ex.get("W", H), ex.get("pad_w", pad)
         P = (H + 2 * pad - R) // stride + 1
-        x = torch.randn(N, H, H, C, device="cuda").bfloat16()
-        g = ConvGeom(stride, pad, pad)
-        flop = 2.0 * N * P * P * K * R * R * C
+        x = torch.randn(N, H, W, C, device="cuda").bfloat16()
+        g = ConvGeom(stride, pad, pad_w)
+        flop = 2.0 * N * P * P * K * R * S * C
         if kind == "fwd":
-            w = (torch.randn(K, R, R, C, device="cuda") * 0.05).bfloat16()
+            w = (torch.randn(K, R, S, C, device="cuda") * 0.05).bfloat16()
             y = torch.empty(N, P, P, K, device="cuda", dtype=torch.bfloat16)
             in_bn = (torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1) if ex.get("pro") else None
             resid = torch.randn(N, P, P, K, device="cuda").bfloat16() if ex.get("res") else None
@@ -104,8 +109,8 @@ def run(only=None, iters=50):
             nbytes = 2 * (x.numel() + w.numel() + y.numel() + (resid.numel() if resid is not None else 0))
         else:
             dy = torch.randn(N, P, P, K, device="cuda").bfloat16()
-            dw = torch.empty(K, R, R, C, device="cuda")
-            ws = torch.empty(be.wgrad_ws_elems(N * P * P, K, R, R, C) or 1, device="cuda")
+            dw = torch.empty(K, R, S, C, device="cuda")
+            ws = torch.empty(be.wgrad_ws_elems(N * P * P, K, R, S, C) or 1, device="cuda")
             a = be.wgrad_args(x, dy, dw, g, ws=ws, target_blocks=ex["target"])
             fn = lambda: _lib_check(be.L.drn_conv_wgrad2(ctypes.byref(a), be.zero_page.data_ptr(), ex["ns"], st))
             nbytes = 2 * (x.numel() + dy.numel()) + 4 * a.splits * dw.numel()
