@@ -202,6 +202,18 @@ __device__ __forceinline__ void store8f(float* p, const float* f) {
   reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
 }
 
+// Per-channel coefficient tables in LDS ([k][C] floats) that every lane reads as its 8-channel
+// group (two ds_read_b128, lanes 32 B apart). Linear, lanes l and l+8 of a 16-lane b128 group
+// hit the same four banks (2-way: VERDICT r5's 73 % SQ_LDS_BANK_CONFLICT of the finalizing BN
+// applies); swapping the two 16-B halves of every odd 64-channel block (channel bit 2 ^= bit 6)
+// makes both reads conflict-free, and the writers' lanes stay a permutation within 8 channels.
+__device__ __forceinline__ int fin_slot(int c) { return c ^ ((c >> 4) & 4); }
+__device__ __forceinline__ void load8f_fin(const float* t, int c, float* f) {
+  const int s = (c >> 4) & 4;  // c is a multiple of 8
+  const float4 a = *reinterpret_cast<const float4*>(t + (c ^ s)), b = *reinterpret_cast<const float4*>(t + ((c + 4) ^ s));
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
 // Per-channel batch statistics -> (scale, shift, mean, invstd) in fp32 (the finalize math).
 __device__ __forceinline__ void bn_stats_to_affine(float s, float q, float count, float gamma, float beta, float eps,
                                                    float& sc, float& sh, float& mean, float& invstd, float& var) {
@@ -425,14 +437,14 @@ __device__ __forceinline__ void bn_bwd_apply_body(DySrc src, const bf16_t* __res
   load8f(shift + c, sh);
   if constexpr (FIN) {
     const bool pub = f.publish && blockIdx.x == 0;
-    for (int cc = threadIdx.x; cc < C; cc += blockDim.x) drn_bn_fin_bwd(f, cc, pub, lsm[cc], lsm[C + cc], lsm[2 * C + cc]);
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      A[j] = lsm[c + j];
-      B[j] = lsm[C + c + j];
-      D[j] = lsm[2 * C + c + j];
+    for (int cc = threadIdx.x; cc < C; cc += blockDim.x) {
+      const int t = fin_slot(cc);
+      drn_bn_fin_bwd(f, cc, pub, lsm[t], lsm[C + t], lsm[2 * C + t]);
     }
+    __syncthreads();
+    load8f_fin(lsm, c, A);
+    load8f_fin(lsm + C, c, B);
+    load8f_fin(lsm + 2 * C, c, D);
   } else {
     // the affine form dx = A*g + B*x + D folds k1*(g - k2 - (x-mu)*is*k3)
     float mu[8], is[8], k1[8], k2[8], k3[8];
@@ -546,16 +558,16 @@ __global__ __launch_bounds__(256) void bn_apply_fin_kernel(const bf16_t* __restr
   extern __shared__ __attribute__((aligned(16))) float lsm[];  // [2][C]
   const int C = CV * 8;
   const bool pub = f.publish && blockIdx.x == 0;
-  for (int c = threadIdx.x; c < C; c += 256) drn_bn_fin_fwd(f, c, pub, lsm[c], lsm[C + c]);
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const int t = fin_slot(c);
+    drn_bn_fin_fwd(f, c, pub, lsm[t], lsm[C + t]);
+  }
   __syncthreads();
   const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int c = (int)(i0 & (CV - 1)) * 8;
   float sc[8], sh[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    sc[j] = lsm[c + j];
-    sh[j] = lsm[C + c + j];
-  }
+  load8f_fin(lsm, c, sc);
+  load8f_fin(lsm + C, c, sh);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const uint4* xv = reinterpret_cast<const uint4*>(x);
   uint4* yv = reinterpret_cast<uint4*>(y);

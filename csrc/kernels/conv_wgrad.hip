@@ -711,6 +711,176 @@ __global__ __launch_bounds__(256) void conv_wgrad_glds_kernel(DrnConvWgradArgs a
 #endif
 }
 
+// ---------------------------------------------------------------------------------------
+// Packed-stem weight gradient from an LDS input halo (the ImageNet 7x7/2 stem in the layout of
+// csrc/kernels/stem.hip: xp[n][h][W + 2][4], filter rows of 8 taps x 4 channels = 32 k).
+// The generic kernel's im2col loader fetches every input piece ~4x per k-tile: a 64-pixel stage
+// is 64 patch rows of 256 B, and adjacent output pixels' 64-byte row segments overlap by 48 B;
+// the kernel is bound by those loads (its loads-only variant runs as long as the kernel itself,
+// profiles/r6_experiments.md). Here a stage is one half output row (QH = Q / 2 <= 61 pixels,
+// padded to 64 MFMA rows): the tile's 4 filter rows of input are loaded ONCE into LDS, 128
+// columns x 8 B = 1 KB per row (one LDS-DMA instruction per row, out-of-image pieces from the zero
+// page), and the transposed fragment reads address the virtual patch image directly: patch
+// (pixel i, k = 32 r + 4 s + c) sits at byte r * 1024 + 16 i + 2 (k mod 32) -- adjacent pixels'
+// patch rows overlap in LDS instead of being fetched again (4 KB of input per stage instead of
+// 16 KB). dY: the stage's QH rows of 128 B (64 channels), loaded and swizzled as by the generic
+// kernel; rows >= QH read the zero page (their patch rows are finite input data, so their
+// products are exact zeros). Grid, splits, slabs and the store are the generic kernel's (2 k-tiles
+// of 128 x channel tiles of 64, split-K over pixels); a split takes the half rows whose first
+// pixel lies in its pixel range, so every pixel is reduced exactly once.
+// ---------------------------------------------------------------------------------------
+template <int NS>
+__global__ __launch_bounds__(256) void stem_wgrad_halo_kernel(DrnConvWgradArgs a, const void* __restrict__ zero) {
+  constexpr int BKK = 128, BCO = 64, BP = 64;
+  constexpr int WB = BCO * 2;                      // dY image row bytes
+  constexpr int A_BYTES = 4 * 1024;                // 4 filter rows x 128 input columns x 8 B
+  constexpr int STAGE = A_BYTES + BP * WB;
+  constexpr int LPB = WB / 16, RIB = 64 / LPB;     // lanes per dY row, dY rows per wave-instruction
+  constexpr int IB = BP / RIB / 4;                 // dY instructions per wave per stage
+  constexpr int G = 1 + IB;                        // LDS-DMA instructions per wave per stage
+  constexpr int D = NS - 1;
+  constexpr int WKK = BKK / 2, WCO = BCO / 2;
+  constexpr int MI = WKK / 16, MJ = WCO / 16;
+  static_assert(NS >= 2 && IB >= 1, "geometry");
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Ktot = a.R * a.S * a.C;
+  const int M = a.N * a.P * a.Q;
+  const int QH = a.Q / 2;
+  const int nkt = (Ktot + BKK - 1) / BKK;
+  const int ntile = gridDim.x;
+  const int lin = xcd_remap(blockIdx.x + blockIdx.y * ntile, ntile * gridDim.y);
+  const int tile = lin % ntile, split = lin / ntile;
+  const int kt = tile % nkt, ct = tile / nkt;
+  const int k0 = kt * BKK, c0 = ct * BCO;
+  const int mbeg = split * a.pix_per_split;
+  const int mend = min(M, mbeg + a.pix_per_split);
+  const int hbeg = (mbeg + QH - 1) / QH, hend = (mend + QH - 1) / QH;
+  const int T = hend > hbeg ? hend - hbeg : 0;
+  const bf16_t* __restrict__ xg = reinterpret_cast<const bf16_t*>(a.x);
+  const bf16_t* __restrict__ dyg = reinterpret_cast<const bf16_t*>(a.dy);
+  // A (input halo): wave w loads filter row r = k0 / 32 + w, lane l the piece at input column
+  // 2 q0 - pad_w + 2 l (two pixels x 4 channels)
+  const int fr = k0 / 32 + wave;
+  // B (dY): as the generic kernel's loader (logical chunk of the lane, swizzle of its rows)
+  const int brow = lane / LPB;
+  int blc;
+  {
+    const int pc = lane % LPB;
+    blc = 2 * ((pc >> 1) ^ slot_swz<WB>(RIB * wave + brow)) + (pc & 1);
+  }
+  const int dc = c0 + blc * 8;
+  const bool cvalid = dc < a.K;
+
+  auto issue = [&](int slot, int hr) {
+    char* st = smem + slot * STAGE;
+    const int np = hr >> 1, hf = hr & 1;
+    const int n = np / a.P, p = np - n * a.P;
+    const int q0 = hf * QH;
+    const int h = p * a.stride - a.pad_h + fr;
+    const int col = q0 * a.stride - a.pad_w + 2 * lane;
+    const bool ok = fr < a.R && (unsigned)h < (unsigned)a.H && col >= 0 && col + 1 < a.W;
+    const bf16_t* src = xg + ((size_t)(n * a.H + h) * a.W + col) * a.C;
+    __builtin_amdgcn_global_load_lds((wg_gbl_void*)(ok ? (const void*)src : zero), (wg_lds_void*)(st + wave * 1024),
+                                     16, 0, 0);
+    const int m0 = np * a.Q + q0;
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int r0 = RIB * (wave + 4 * i);
+      const bool okb = cvalid && r0 + brow < QH && m0 + r0 + brow < M;
+      const bf16_t* bs = dyg + (size_t)(m0 + r0 + brow) * a.K + dc;
+      __builtin_amdgcn_global_load_lds((wg_gbl_void*)(okb ? (const void*)bs : zero),
+                                       (wg_lds_void*)(st + A_BYTES + r0 * WB), 16, 0, 0);
+    }
+  };
+
+  f32x4_t acc[MI][MJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  const int wk = wave & 1, wc = wave >> 1;
+  const uint32_t lds_base = (uint32_t)reinterpret_cast<uintptr_t>(smem);
+  // fragment addresses: A (virtual patch image) row = pixel 8g + q4 (+4, +32 ks: immediates),
+  // columns k = wk * WKK + 16 i + 4 p4 .. +3 (inside one 32-k filter row)
+  uint32_t a_lane[MI], b_lane[MJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int kl = wk * WKK + 16 * i + 4 * p4;
+    a_lane[i] = (uint32_t)((kl >> 5) * 1024 + 2 * (kl & 31) + 16 * (8 * g + q4));
+  }
+#pragma unroll
+  for (int j = 0; j < MJ; ++j) b_lane[j] = (uint32_t)swz_off<WB>(8 * g + q4, wc * WCO + 16 * j + 4 * p4);
+
+#pragma unroll
+  for (int s = 0; s < D; ++s)
+    if (s < T) issue(s, hbeg + s);
+
+  for (int t = 0; t < T; ++t) {
+    if (t + D - 1 < T) wg_wait_vmcnt<G * (D - 1)>();
+    else wg_wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + D < T) issue((t + D) % NS, hbeg + t + D);
+    const uint32_t cur = lds_base + (uint32_t)((t % NS) * STAGE);
+    uint32_t ba[MI], bb[MJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) ba[i] = cur + a_lane[i];
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) bb[j] = cur + b_lane[j];
+    s16x4v fa[2][MI][2], fb[2][MJ][2];
+    static_for<0, 2>([&](auto KSI) {
+      constexpr int ks = decltype(KSI)::value;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        fa[ks][i][0] = tr_read_asm<16 * (32 * ks)>(ba[i]);
+        fa[ks][i][1] = tr_read_asm<16 * (32 * ks + 4)>(ba[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < MJ; ++j) {
+        fb[ks][j][0] = tr_read_asm<A_BYTES + (32 * ks) * WB>(bb[j]);
+        fb[ks][j][1] = tr_read_asm<A_BYTES + (32 * ks + 4) * WB>(bb[j]);
+      }
+    });
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      if (ks == 0) lgkm_fence<2 * (MI + MJ)>(fa[0], fb[0]);
+      else lgkm_fence<0>(fa[1], fb[1]);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < MJ; ++j) {
+          const bf16x8_t af = __builtin_bit_cast(
+              bf16x8_t, __builtin_shufflevector(fa[ks][i][0], fa[ks][i][1], 0, 1, 2, 3, 4, 5, 6, 7));
+          const bf16x8_t bfr = __builtin_bit_cast(
+              bf16x8_t, __builtin_shufflevector(fb[ks][j][0], fb[ks][j][1], 0, 1, 2, 3, 4, 5, 6, 7));
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[i][j], 0, 0, 0);
+        }
+    }
+    asm volatile("" ::: "memory");
+  }
+  wgrad_store<MI, MJ>(a, acc, split, c0 + wc * WCO, k0 + wk * WKK, Ktot, lane);
+}
+
+template <int NS>
+static int launch_stem_wgrad_halo(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
+  constexpr int LDS = NS * (4 * 1024 + 64 * 64 * 2);
+  const int Ktot = a->R * a->S * a->C;
+  drn::launch(stem_wgrad_halo_kernel<NS>, dim3(((Ktot + 127) / 128) * ((a->K + 63) / 64), a->splits), dim3(256), LDS,
+              s, *a, zero);
+  return (int)hipGetLastError();
+}
+
+// the packed-stem geometry the halo kernel covers (host check)
+static bool stem_halo_ok(const DrnConvWgradArgs* a, const void* zero) {
+  const int QH = a->Q / 2;
+  return zero != nullptr && a->C == 4 && a->S == 8 && a->R <= 8 && a->stride == 2 && a->pad_w % 2 == 0 &&
+         a->Q % 2 == 0 && QH >= 1 && 2 * QH + a->S - 2 <= 128 && a->K % 64 == 0 && a->in_scale == nullptr &&
+         a->splits >= 1 && a->pix_per_split % 64 == 0;
+}
+
 template <int BKK, int BCO, int NS, int BP, bool PRO, bool IL = false, bool LIN = false>
 static int launch_wgrad_glds_p(DrnConvWgradArgs* a, const void* zero, hipStream_t s) {
   constexpr int LDS = NS * (BP * BKK * 2 + BP * BCO * 2);
@@ -872,13 +1042,18 @@ DRN_API int drn_conv_wgrad(DrnConvWgradArgs* a, hipStream_t s) {
   return a->in_scale != nullptr ? drn::dispatch_wgrad<true>(a, s) : drn::dispatch_wgrad<false>(a, s);
 }
 
-// LDS-DMA wgrad (no prologue); ns = pipeline stages (2 or 3), 0 = register-staged kernel.
+// LDS-DMA wgrad; ns = pipeline (dispatch_wgrad_glds), 0 = register-staged kernel, 9 / 10 = the
+// packed stem's input-halo kernel with 3 / 4 stages.
 DRN_API int drn_conv_wgrad2(DrnConvWgradArgs* a, const void* zero, int ns, hipStream_t s) {
   // C == 4: the packed stem (stem.hip) -- every 16-byte k piece is a tap pair x 4 channels, so the
   // tap count must be even (S padded to 8); LDS-DMA kernels, no fused prologue
   const bool packed = a->C == 4 && a->S % 2 == 0 && a->in_scale == nullptr && zero != nullptr && ns != 0;
   if (((a->C % 8) != 0 && !packed) || (a->K % 8) != 0 || a->splits < 1 || (a->pix_per_split % 64) != 0)
     return (int)hipErrorInvalidValue;
+  if (ns == 9 || ns == 10) {  // packed-stem input halo (3 / 4 stages)
+    if (!drn::stem_halo_ok(a, zero)) return (int)hipErrorInvalidValue;
+    return ns == 9 ? drn::launch_stem_wgrad_halo<3>(a, zero, s) : drn::launch_stem_wgrad_halo<4>(a, zero, s);
+  }
   // (the LDS-DMA kernels' fused BN prologue always applies the ReLU: pre-activation v2)
   if (zero == nullptr || ns == 0 || (a->in_scale != nullptr && a->relu_in == 0)) return drn_conv_wgrad(a, s);
   return drn::dispatch_wgrad_glds(a, zero, ns, s);

@@ -602,11 +602,12 @@ class HipBackend(_Common):
     def _tune_wgrad(self, args_for, out, key, iters: int = 0) -> tuple:
         """Pick (split-K target, pipeline) by timing the weight-gradient kernel TOGETHER with its
         split-K reduction: 0 = register-staged, 2/3 = LDS-DMA stages of 64 pixels, 4/5/6 = 2/3/4
-        stages of 32 pixels. Writes only the workspace and this gradient slot (rewritten by the
+        stages of 32 pixels, 7/8 = the interleaved-issue 64-pixel pipelines, 9/10 = the packed
+        stem's input-halo kernel with 3/4 stages (other geometries refuse it). Writes only the workspace and this gradient slot (rewritten by the
         real launch that follows)."""
         iters = iters or self.tune_iters
         st = self.stream()
-        cands = tuple(int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6,7,8").split(","))
+        cands = tuple(int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6,7,8,9,10").split(","))
         seen = set()
         modes = (False, True) if self.wgrad_atomic_ok else (False,)
 
@@ -654,7 +655,7 @@ class HipBackend(_Common):
             raise RuntimeError(f"untuned weight gradient {key} while recording a step (tune it eagerly first)")
         if key not in self.wgrad_ns and self.autotune and not torch.cuda.is_current_stream_capturing():
             hit = self.tune_db().get_wgrad(key)
-            cands = [int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6,7,8").split(",")]
+            cands = [int(c) for c in os.environ.get("DRN_WGRAD_CANDS", "0,2,3,4,5,6,7,8,9,10").split(",")]
             if hit is not None and (not hit[2] or self.wgrad_atomic_ok) and hit[1] in cands:
                 self.db_hits += 1
                 self.wgrad_ns[key] = hit

@@ -52,6 +52,10 @@ CASES = {
     # input [N][224][226][4], taps 7 x 8 (the 8th tap zero), pad (3, 2); the last kernel of the step
     "fwd_stem": ("fwd", 128, 224, 4, 64, 7, 2, 3, dict(cfg=12, S=8, W=226, pad_w=2)),
     "wgrad_stem": ("wgrad", 128, 224, 4, 64, 7, 2, 3, dict(ns=2, target=512, S=8, W=226, pad_w=2)),
+    # ... and by the input-halo kernel (conv_wgrad.hip stem_wgrad_halo_kernel, 3 / 4 stages)
+    "wgrad_stem_halo3": ("wgrad", 128, 224, 4, 64, 7, 2, 3, dict(ns=9, target=512, S=8, W=226, pad_w=2)),
+    "wgrad_stem_halo4": ("wgrad", 128, 224, 4, 64, 7, 2, 3, dict(ns=10, target=512, S=8, W=226, pad_w=2)),
+    "wgrad_stem_halo3_768": ("wgrad", 128, 224, 4, 64, 7, 2, 3, dict(ns=9, target=768, S=8, W=226, pad_w=2)),
 }
 # --sweep: the 3x3 forward shapes under other tile / pipeline configurations (name@cfg)
 SWEEP = {"fwd3x3_28": (1, 2, 8, 9, 17, 20, 27, 30, 31), "fwd3x3_14": (1, 2, 8, 9, 17, 20, 25, 26, 29, 30)}
