@@ -62,7 +62,7 @@ def main():
     result_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
 
-    import distributed_resnet_tensorflow_amd  # noqa: F401 -- its HIP queue default (GPU_MAX_HW_QUEUES) precedes HIP init
+    import distributed_resnet_tensorflow_amd  # noqa: F401 -- (package-level process settings precede HIP init)
     import torch
     import torch.distributed as dist
 
@@ -98,11 +98,12 @@ def main():
         # parallel.engine.use_priority_main_stream
         from distributed_resnet_tensorflow_amd.parallel.engine import use_priority_main_stream
         use_priority_main_stream()
-    elif args.graph == -1 and not (world > 1 or force_dp):
+    elif args.graph == -1 and (p2p or not (world > 1 or force_dp)):
         # auto on one GPU: the EAGER candidate runs on a high-priority main stream too (ResNet-50
         # bs128, one box: 9.92-9.94 ms vs 10.15-10.19 ms on the normal-priority stream,
         # profiles/r3_side_stream_ab.txt); the HIP-graph candidate is captured and replayed from
-        # a normal-priority stream (replay from a high-priority one measured far slower)
+        # a normal-priority stream (replay from a high-priority one measured far slower); the
+        # same for the P2P data-parallel step (graph vs eager vs native plan)
         from distributed_resnet_tensorflow_amd.parallel.engine import make_priority_stream
         prio = make_priority_stream()
     if world > 1 or force_dp:
@@ -199,7 +200,7 @@ def main():
     use_graph = args.graph if args.graph >= 0 else int(eng is None or eng.p2p is not None)
     if eng is not None and eng.zero1:
         use_graph = 0
-    want_plan = args.plan != 0 and (eng is None or (eng.p2p is None and not eng.zero1 and eng.mode == "sync"))
+    want_plan = args.plan != 0 and (eng is None or (not eng.zero1 and eng.mode == "sync"))
     cands, mode_times, plan = {}, None, None
 
     def in_eager_ctx(fn):
@@ -243,11 +244,11 @@ def main():
                 plan.replay()
             cands["plan"] = in_eager_ctx(plan_1t)
             cands["plan_threads"] = in_eager_ctx(plan_mt)
-            if eng is None and args.plan != 1:
+            if (eng is None or eng.p2p is not None) and args.plan != 1:
                 # ... and a plan recorded without the side stream (small steps)
                 side, ex.side = ex.side, None
                 with torch.cuda.stream(prio) if prio is not None else torch.cuda.stream(torch.cuda.current_stream()):
-                    plan1 = StepPlan(ex, None, warmup=1)
+                    plan1 = StepPlan(ex, eng, grad_scale=1.0 / world, warmup=1)
                 ex.side = side
                 cands["plan_one_stream"] = in_eager_ctx(plan1.replay)
                 one_stream["plan_one_stream"] = True

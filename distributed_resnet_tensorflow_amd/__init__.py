@@ -1,12 +1,8 @@
 """drn: MI355X-native distributed ResNet training (see README.md)."""
-import os as _os
-
-# One hardware queue per HIP stream. HIP's default (GPU_MAX_HW_QUEUES=4) maps the fourth
-# normal-priority stream of a process onto a queue another stream already uses, and the two are
-# then serialised behind each other's cross-stream waits. The data-parallel step with the ImageNet
-# feeder has four (weight-gradient side stream, RCCL's stream, the bucket-report stream, the H2D
-# copy stream): its native plan ran 15.0-15.2 ms per step with 4 queues and 10.0 ms with 8, the
-# same step without the feeder 9.9-10.0 ms (scripts/imagenet_copy_stream_probe.py,
-# profiles/r6_imagenet_copy_stream.jsonl). Read when HIP initialises, so this must precede the
-# first GPU call; an explicit setting wins.
-_os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# Hardware queues: the package keeps HIP's default (GPU_MAX_HW_QUEUES=4 normal-priority queues
+# per process) and instead keeps the number of busy normal-priority streams within it (the
+# ImageNet feeder's H2D copy stream is high-priority: train/feeder.py). Raising the queue count
+# was measured and rejected: with 5, 6 or 8 queues some multi-stream step modes fall into 3-5x
+# slower steps (queues time-sliced, kernels and cross-queue waits stretched: CIFAR ResNet-50 bs32
+# whole-step graph 4.7-6.3 ms and P2P native plan 8.6-9.4 ms vs 1.8-1.9 ms with 4 queues,
+# profiles/r6_p2p_plan_queues.txt).

@@ -210,8 +210,8 @@ class DataParallelEngine:
         self._step_no += 1
         if self.watchdog is not None:
             self.watchdog.arm(self._step_no)
-        if self.cuda and torch.cuda.is_current_stream_capturing():
-            self._ev = self._host_t = None     # a whole-step graph capture: no timing events
+        if self.cuda and (torch.cuda.is_current_stream_capturing() or getattr(self.ex.sched, "recording", False)):
+            self._ev = self._host_t = None     # a whole-step graph capture / plan recording: no timing events
         elif self.cuda:
             self._ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             self._ev[0].record()
@@ -224,10 +224,11 @@ class DataParallelEngine:
         else:
             self.ex.grad_ready = None
 
-    def _launch(self, i: int, buf: Optional[torch.Tensor] = None):
+    def _launch(self, i: int, buf: Optional[torch.Tensor] = None, final: bool = False):
         lo, hi = self.buckets[i]
         if self.p2p is not None:
-            self.p2p.reduce_bucket(i, lo, hi)
+            side = self.ex.side
+            self.p2p.reduce_bucket(i, lo, hi, after=(side,) if side is not None else (), final=final)
             self.launched[i] = True
             return
         t = (self.P.grad if buf is None else buf)[lo:hi]
@@ -253,6 +254,13 @@ class DataParallelEngine:
             if not self.launched[i] and lo >= self.frontier:
                 self._launch(i)
 
+    @property
+    def wants_report_stream(self) -> bool:
+        """Whether the executor issues this engine's bucket launches from its report stream
+        (host-issued collectives); the P2P all-reduce orders its comm stream after the compute
+        streams itself (P2PAllReduce.reduce_bucket)."""
+        return self.p2p is None
+
     def launches_at(self, lo_ready: int) -> bool:
         """Whether a grad_ready(lo_ready) report would launch a bucket (the executor orders the
         report after the main stream only then: a report that launches nothing needs no
@@ -276,7 +284,7 @@ class DataParallelEngine:
         if self.mode == "sync":
             for i in range(len(self.buckets)):
                 if not self.launched[i]:
-                    self._launch(i)
+                    self._launch(i, final=True)
             self._mark(1)                      # backward done (all buckets issued)
             for w in self.works:
                 w.wait()

@@ -136,6 +136,7 @@ class P2PAllReduce:
     """Maps every rank's `grad` (and flag words) and reduces buckets of it into `out`."""
 
     _count = 0
+    INLINE_MAX_MB = 16
 
     def __init__(self, grad: torch.Tensor, group=None, two_shot_min_kb: int = -1, wire: str = ""):
         P2PAllReduce._count += 1
@@ -151,6 +152,18 @@ class P2PAllReduce:
         self.grad = grad
         self._arg_cache = {}
         self.comm = torch.cuda.Stream(device=grad.device)
+        # Where the bucket reductions run. On the P2P comm stream they overlap the rest of the
+        # backward pass, but every bucket then costs two cross-queue hand-offs (compute -> comm ->
+        # compute): CIFAR ResNet-50 bs32 at world 1, 1.85-1.94 ms per step vs 1.61 ms with the
+        # reductions on the compute stream itself, i.e. the single-GPU rate 1.59 ms
+        # (profiles/r6_p2p_plan_queues.txt). A small gradient's buckets reduce in microseconds and
+        # the peers reach them together, so "auto" runs them inline up to INLINE_MAX_MB of
+        # gradient; larger ones keep the comm stream (DRN_P2P_INLINE=auto | 1 | 0).
+        mode = os.environ.get("DRN_P2P_INLINE", "auto").lower()
+        self.inline = (mode == "1") or (mode == "auto" and grad.numel() * 4 <= self.INLINE_MAX_MB * (1 << 20))
+        # cross-stream ordering: torch's stream API, or a native plan's recorder while a StepPlan
+        # records the step (runtime/plan.py: the bucket kernels are then replayed from C++ too)
+        self.sched = None
         dev = grad.device
         self.two_shot_min = 1024 * (two_shot_min_kb if two_shot_min_kb >= 0 else
                                     int(os.environ.get("DRN_P2P_TWO_SHOT_MIN_KB", "1024")))
@@ -236,29 +249,39 @@ class P2PAllReduce:
         _lib.check(self.L.drn_p2p_step(ctypes.byref(a), ctypes.c_void_p(self.epoch.data_ptr()), self._stream()),
                    "drn_p2p_step")
 
-    def reduce_bucket(self, i: int, lo: int, hi: int):
-        """Bucket i = grad[lo:hi] is complete on the current stream: (bf16 wire: cast it to the
-        shadow there) then ONE kernel on the comm stream publishes it, polls for the peers without
-        blocking the rest of this rank's backward pass, and reduces."""
+    def reduce_bucket(self, i: int, lo: int, hi: int, after=(), final: bool = False):
+        """Bucket i = grad[lo:hi] is complete on the current stream and on the `after` streams
+        (the executor's weight-gradient side stream): the comm stream waits for all of them, then
+        (bf16 wire: casts the bucket to the shadow and) ONE kernel publishes it, polls for the
+        peers without blocking the rest of this rank's backward pass, and reduces. No separate
+        report stream: every stream a step uses is one more hardware queue, and with short CIFAR
+        kernels each extra queue's cross-stream waits cost (profiles/r6_p2p_plan_queues.txt).
+        final: a bucket launched after the backward pass (engine.finish) runs on the current
+        stream itself -- nothing is left to overlap with, and the optimizer right behind it is
+        then not two cross-queue hand-offs (there and back) away from its input."""
         assert (hi - lo) % 4 == 0 and lo % 4 == 0 and i + 1 < N_SLOTS
         if i == self.withhold:
             return  # fault injection: this rank never publishes bucket i
         a = self._args(lo, hi, i + 1)
         cur = torch.cuda.current_stream()
+        st = cur if (final or self.inline) else self.comm
+        if st is not cur:
+            self._wait_stream(st, cur)
+        for s in after:
+            self._wait_stream(st, s)
         bf16 = self.shadow is not None
         if bf16:
             _lib.check(self.L.drn_p2p_cast(ctypes.c_void_p(self.grad.data_ptr() + lo * 4),
                                            ctypes.c_void_p(self.shadow.data_ptr() + lo * 2), hi - lo,
-                                           cur.cuda_stream), "drn_p2p_cast")
-        self.comm.wait_stream(cur)
+                                           st.cuda_stream), "drn_p2p_cast")
         # at most 128 workgroups: a reduce waiting for a slow peer must leave most CUs to this
         # rank's own backward kernels (which publish the later buckets the peers wait for)
         blocks = max(1, min(128, (hi - lo) // 4 // 256))
         if (hi - lo) * 4 >= self.two_shot_min and self.world > 1:
-            _lib.check(self.L.drn_p2p_reduce2(ctypes.byref(a), blocks, int(bf16), self.comm.cuda_stream),
+            _lib.check(self.L.drn_p2p_reduce2(ctypes.byref(a), blocks, int(bf16), st.cuda_stream),
                        "drn_p2p_reduce2")
         else:
-            _lib.check(self.L.drn_p2p_reduce(ctypes.byref(a), blocks, int(bf16), self.comm.cuda_stream),
+            _lib.check(self.L.drn_p2p_reduce(ctypes.byref(a), blocks, int(bf16), st.cuda_stream),
                        "drn_p2p_reduce")
 
     def end_step(self):
@@ -266,8 +289,16 @@ class P2PAllReduce:
         DONE publish happens at the next step's boundary launch) and queue the copy of the error
         word into pinned host memory (read by poll() without a device sync)."""
         cur = torch.cuda.current_stream()
-        cur.wait_stream(self.comm)
-        self.err_host.copy_(self.err, non_blocking=True)
+        if not self.inline:
+            self._wait_stream(cur, self.comm)
+        if self.sched is None:          # (a replayed plan queues the copy itself: StepPlan.replay)
+            self.err_host.copy_(self.err, non_blocking=True)
+
+    def _wait_stream(self, dst, src):
+        if self.sched is None:
+            dst.wait_stream(src)
+        else:
+            self.sched.wait_stream(dst, src)
 
     @staticmethod
     def _raise(e: int):

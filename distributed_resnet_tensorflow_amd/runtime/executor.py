@@ -735,9 +735,9 @@ class Executor:
         stream at every launching report, stalling the next blocks' weight gradients)."""
         if self.grad_ready is None:
             return
-        if self.sched.recording:                         # a native plan is cut here: the report
-            self.sched.cut(("report", lo))               # runs from Python at each replay
-            return
+        if self.sched.recording and not getattr(self.sched, "native_reports", False):
+            self.sched.cut(("report", lo))               # a native plan is cut here: the report
+            return                                       # runs from Python at each replay
         if self.side is None:
             self.grad_ready(lo)
             return
@@ -745,12 +745,16 @@ class Executor:
         if owner is not None and hasattr(owner, "launches_at") and not owner.launches_at(lo):
             self.grad_ready(lo)                          # (advances the frontier, launches nothing)
             return
+        if not getattr(owner, "wants_report_stream", True):
+            self.grad_ready(lo)                          # (P2P: its comm stream waits on both streams)
+            return
         main = torch.cuda.current_stream(self.device)
         if self._report_stream is None:
             self._report_stream = torch.cuda.Stream(self.device)
         rs = self._report_stream
-        rs.wait_stream(main)                             # readiness event of the main-stream producers
-        rs.wait_stream(self.side)                        # ... and of the weight gradients
+        self.sched.wait_stream(rs, main)                 # readiness event of the main-stream producers
+        self.sched.wait_stream(rs, self.side)            # ... and of the weight gradients
+        # (P2P engine under a plan recording: the bucket kernels below are recorded into the plan)
         with torch.cuda.stream(rs):
             self.grad_ready(lo)
         self._reported = True
@@ -801,7 +805,7 @@ class Executor:
             return
         main = torch.cuda.current_stream(self.device)
         if self._reported:                               # (a capture must rejoin every forked stream)
-            main.wait_stream(self._report_stream)
+            self.sched.wait_stream(main, self._report_stream)
             self._reported = False
         if ev is None:
             self.sched.wait_stream(main, self.side)

@@ -13,7 +13,11 @@ record / stream wait entries instead of torch's stream API). `replay()` re-issue
 `drn_plan_replay` -- the same kernels, arguments, streams and priorities as the eager step, one
 host call per segment. Data-parallel steps over RCCL are cut where the eager step hands a bucket
 to the engine: at replay, each cut runs the engine's Python side (begin_step, the bucket
-collectives issued from the report stream, finish) between two native segments.
+collectives issued from the report stream, finish) between two native segments. With the P2P
+all-reduce (parallel/p2p.py) every collective is a library kernel synchronised by device-side
+epoch flags, so the step boundary, the bf16 wire casts, the bucket reductions on the P2P comm
+stream and their cross-stream ordering are recorded too: the data-parallel step is ONE native
+segment (the CIFAR 4-GPU configuration; before, P2P steps could only be one HIP graph).
 
 The reference's counterpart is the TF1 C++ executor running the captured train_op every
 `mon_sess.run` (resnet_cifar_main.py:320-321).
@@ -116,8 +120,9 @@ class StepPlan:
     def __init__(self, ex, engine=None, grad_scale: float = 1.0, warmup: int = 1, threads: int = 1):
         self.L = _lib.lib()
         self.ex, self.eng, self.grad_scale = ex, engine, grad_scale
-        if engine is not None and (engine.p2p is not None or engine.mode != "sync" or engine.zero1):
-            raise ValueError("native plans cover the synchronous, unsharded RCCL / gloo engine (P2P: one HIP graph)")
+        if engine is not None and (engine.mode != "sync" or engine.zero1):
+            raise ValueError("native plans cover the synchronous, unsharded data-parallel engine")
+        self.p2p = engine.p2p if engine is not None else None
         for _ in range(warmup):         # kernel attributes, workspaces, tuning: all outside the plan
             self._eager()
         torch.cuda.synchronize()
@@ -127,7 +132,10 @@ class StepPlan:
         be = ex.be
         sched, old = PlanSched(self), ex.sched
         ex.sched, be.recording = sched, True
-        if engine is not None:
+        if self.p2p is not None:
+            sched.native_reports = True       # (the executor issues the bucket kernels while recording)
+            self.p2p.sched = sched
+        elif engine is not None:
             ex.grad_ready = lambda lo: None   # (reports become plan cuts: PlanSched.cut)
         _lib.check(self.L.drn_plan_record_begin(self.p), "drn_plan_record_begin")
         ok = False
@@ -136,6 +144,11 @@ class StepPlan:
             if engine is None:
                 ex.backward(defer_tail=not ex.check_nan)
                 ex.apply_gradients()
+            elif self.p2p is not None:
+                engine.begin_step()
+                ex.backward()
+                self._grad = engine.finish()
+                engine.apply_gradients(self._grad, grad_scale)
             else:
                 self._cut("begin")
                 ex.backward()
@@ -147,6 +160,8 @@ class StepPlan:
             self.L.drn_plan_record_end()
             ex.sched, be.recording = old, False
             ex.grad_ready = None
+            if self.p2p is not None:
+                self.p2p.sched = None
             if not ok:
                 # a failed recording leaves plan events in the executor's carry-over state: the
                 # next eager step would hand them to torch's stream API
@@ -200,6 +215,15 @@ class StepPlan:
 
     def replay(self):
         L, p, ex, eng = self.L, self.p, self.ex, self.eng
+        if self.p2p is not None:
+            # one segment; the host side of the step is the engine's replay bookkeeping and the
+            # error word's copy into pinned memory (P2PAllReduce.end_step, eager)
+            eng.replay_begin()
+            _lib.check(L.drn_plan_replay(p, 0, self.cuts[-1][0]), "drn_plan_replay")
+            self.p2p.err_host.copy_(self.p2p.err, non_blocking=True)
+            eng.replay_end()
+            self._after_replay()
+            return
         begin = 0
         for end, action in self.cuts:
             if end > begin:
@@ -214,7 +238,11 @@ class StepPlan:
                 assert g is self._grad, "the recorded update reads a different gradient buffer"
             else:                       # ("report", lo): the bucket collectives, live
                 ex._report(action[1])
-        if eng is None:
+        self._after_replay()
+
+    def _after_replay(self):
+        ex = self.ex
+        if self.eng is None:
             ex._tail_ev = None          # (the recorded step joined its deferred tail itself)
         if self._tflip and ex.side is not None:
             # the replay ended with the data-gradient weight refresh on the side stream: an eager

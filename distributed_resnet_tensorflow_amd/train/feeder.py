@@ -8,6 +8,8 @@ Synthetic mode fills the device batch once (benchmarks: BASELINE "synthetic data
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -64,18 +66,22 @@ class _StagedFeeder:
     streams) shares one of the GPU_MAX_HW_QUEUES=4 hardware queues with a compute stream, and the
     cross-stream waits then serialise them: the CIFAR ResNet-50 bs32 CLI over RCCL ran 9.15 ms per
     step with the copy stream vs 2.05 ms without it, single-GPU 1.92 vs 1.81 ms
-    (profiles/r5_cli_step_rate.txt). On for ImageNet, whose tens of MB per batch must overlap; the
-    hardware-queue sharing itself is gone since the package sets GPU_MAX_HW_QUEUES=8 (one queue
-    per stream): the ImageNet data-parallel step with this copy stream 10.0-10.1 ms vs 15.0-15.2 ms
-    with 4 queues, and 11.5 ms with the copies on the consuming stream
-    (profiles/r6_imagenet_copy_stream.jsonl).
+    (profiles/r5_cli_step_rate.txt). On for ImageNet, whose tens of MB per batch must overlap,
+    as a HIGH-priority stream (COPY_STREAM_PRIORITY, DRN_COPY_STREAM_PRIORITY): that pool holds
+    only the critical-path stream, so the copy stream shares no queue with a normal-priority
+    compute stream. The ImageNet data-parallel step with the feeder: 10.09-10.10 ms vs 11.6 ms
+    with a normal-priority copy stream (15.0-15.5 ms as a native plan) and 9.93 ms without
+    copies (scripts/imagenet_copy_stream_probe.py, profiles/r6_imagenet_copy_stream.jsonl).
     """
     COPY_STREAM = True
+    COPY_STREAM_PRIORITY = -1
 
     def _init_staging(self, ex):
         self.ex = ex
         self.gpu = ex.device.type == "cuda"
-        self.copy_stream = torch.cuda.Stream(device=ex.device) if self.gpu and self.COPY_STREAM else None
+        prio = int(os.environ.get("DRN_COPY_STREAM_PRIORITY", str(self.COPY_STREAM_PRIORITY)))
+        self.copy_stream = (torch.cuda.Stream(device=ex.device, priority=prio)
+                            if self.gpu and self.COPY_STREAM else None)
         self._pending = None
         self._consumed = None          # event after the preprocess of the batch last handed out
         self._main = None              # the stream that consumes the batches (set by next())

@@ -130,15 +130,20 @@ class TrainingSession:
         dp_graph = os.environ.get("DRN_DP_GRAPH", "auto")
         hip_cuda = self.device.type == "cuda" and self.be.name == "hip"
         # (step_trial=False: a single-GPU session keeps the whole-step graph without timing it)
+        # data parallel over P2P: the whole-step graph and the native plan (P2P kernels recorded,
+        # runtime/plan.py) are timed against each other, like the single-GPU step
+        p2p_trial = (use_graph and hip_cuda and dp_ok and self.engine.p2p is not None and dp_graph == "auto"
+                     and step_trial)
         self.use_graph = use_graph and hip_cuda and (
-            (dp_ok and self.engine.p2p is not None) or (dp_ok and dp_graph == "1") or (not dp and not step_trial))
+            (dp_ok and self.engine.p2p is not None and not p2p_trial) or (dp_ok and dp_graph == "1")
+            or (not dp and not step_trial))
         # step-mode trial of the RCCL data-parallel step: eager, native plan, segmented graphs;
         # of the single-GPU step: the whole-step graph (then its side-stream trial) or the native
         # plan (ImageNet ResNet-50 bs128: plan 9.75 vs graph 10.52 ms, profiles/r5_bench_modes_v1.jsonl)
         modes = None
         if use_graph and hip_cuda and dp_ok and self.engine.p2p is None and dp_graph == "auto":
             modes = ["eager", "plan", "graph"]
-        elif use_graph and hip_cuda and not dp and step_trial:
+        elif (use_graph and hip_cuda and not dp and step_trial) or p2p_trial:
             # (+ the plan recorded without the weight-gradient side stream: small steps, e.g. CIFAR
             # ResNet-50 bs32: bench 1.59 ms one-stream vs 1.70 ms two-stream plan)
             modes = ["graph", "plan"] + (["plan_one_stream"] if self.ex.side is not None else [])
@@ -152,7 +157,7 @@ class TrainingSession:
         self._strial = None
         # (also for the data-parallel P2P graph step: its reductions run on the P2P comm stream
         # either way, only the weight gradients move)
-        self._side_trial = ((self.use_graph or (self._trial is not None and self.engine is None))
+        self._side_trial = ((self.use_graph or self._trial is not None)
                             and (self.engine is None or self.engine.p2p is not None)
                             and self.ex.side is not None and os.environ.get("DRN_SIDE_TRIAL", "1") == "1")
         self.side_choice: Optional[dict] = None
@@ -320,13 +325,13 @@ class TrainingSession:
             torch.cuda.synchronize(self.device)
             side, self.ex.side = self.ex.side, None
             try:
-                self._plan1 = StepPlan(self.ex, None, warmup=1)
+                self._plan1 = StepPlan(self.ex, self.engine, 1.0 / self.world, warmup=1)
             finally:
                 self.ex.side = side
             return
         if mode == "graph" and self._graph is None:
             torch.cuda.synchronize(self.device)
-            if self.engine is None:
+            if self.engine is None or self.engine.p2p is not None:
                 self._graph = self._on_graph_stream(lambda: StepGraph(self._step_body, warmup=1))
             else:
                 self._graph = self._on_graph_stream(
@@ -349,7 +354,7 @@ class TrainingSession:
         ms = agree_ms([tr["ms"][m] for m in modes], getattr(self.engine, "group", None))  # same mode everywhere
         pick = modes[min(range(len(modes)), key=lambda i: ms[i])]
         self.graph_choice = {f"{m}_ms": round(v, 3) for m, v in zip(modes, ms)}
-        graph_name = "segmented graphs" if self.engine is not None else "graph"
+        graph_name = "segmented graphs" if self.engine is not None and self.engine.p2p is None else "graph"
         self.graph_choice["mode"] = {"graph": graph_name, "plan": "native plan",
                                      "plan_one_stream": "native plan (one stream)"}.get(pick, "eager")
         log.info("%s step: %s -> %s", "data-parallel" if self.engine is not None else "single-GPU",
@@ -360,7 +365,7 @@ class TrainingSession:
             self._graph = None
         else:
             self.use_graph = True
-            if self._side_trial and self.engine is None:
+            if self._side_trial:
                 # the whole-step graph: its side-stream trial follows (_side_trial_tick)
                 self._strial = ["side", 0, 0.0, 0.0, None, None, 0.0]
         if pick == "plan_one_stream":

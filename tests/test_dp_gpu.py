@@ -44,6 +44,9 @@ def _worker(rank, world, port, q, allreduce="rccl"):
         if allreduce == "p2p2":           # two-shot for every bucket
             os.environ["DRN_P2P_TWO_SHOT_MIN_KB"] = "0"
             allreduce = "p2p"
+        if allreduce == "p2pc":           # reductions on the P2P comm stream (not inline)
+            os.environ["DRN_P2P_INLINE"] = "0"
+            allreduce = "p2p"
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2
@@ -84,7 +87,7 @@ def _worker(rank, world, port, q, allreduce="rccl"):
         q.put((rank, repr(e) + traceback.format_exc(), False))
 
 
-@pytest.mark.parametrize("allreduce", ["rccl", "p2p", "p2p2", "rcclb", "p2pb", "p2p2b"])
+@pytest.mark.parametrize("allreduce", ["rccl", "p2p", "p2p2", "p2pc", "rcclb", "p2pb", "p2p2b"])
 def test_dp_engine_gpu_two_ranks_one_device(allreduce):
     """rccl here means the engine's torch.distributed path (gloo on this one-GPU box); p2p is
     the one-shot HIP-IPC kernel path (parallel/p2p.py) with its device-side epoch flags, p2p2
@@ -360,6 +363,93 @@ def test_graph_captured_dp_p2p_step_bitwise_equals_eager():
     for rank, bitwise, same in res:
         assert bitwise is True, (rank, bitwise)
         assert same
+
+
+def _plan_p2p_worker(rank, world, port, q, threads, wire, inline):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DRN_DETERMINISTIC="1",
+                          DRN_P2P_INLINE=inline)
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from distributed_resnet_tensorflow_amd.models.spec import cifar_resnet_v2
+        from distributed_resnet_tensorflow_amd.ops.backend import HipBackend
+        from distributed_resnet_tensorflow_amd.parallel.engine import DataParallelEngine
+        from distributed_resnet_tensorflow_amd.runtime.plan import StepPlan
+        spec, N = cifar_resnet_v2(8), 8
+        be = HipBackend("cuda")                 # one backend: identical kernel configurations
+        exs, engs = [], []
+        for _ in range(2):
+            ex = _make(spec, N, rank, seed=1 + rank, be=be)
+            ex.set_lr(0.1)
+            eng = DataParallelEngine(ex, bucket_mb=0.05, allreduce="p2p", wire=wire)
+            assert eng.p2p is not None and len(eng.buckets) > 1
+            eng.broadcast_parameters()
+            exs.append(ex)
+            engs.append(eng)
+        ex, eng = exs[0], engs[0]
+        for _ in range(4):                      # eager reference: 4 data-parallel steps
+            ex.forward(True)
+            eng.begin_step()
+            ex.backward()
+            eng.apply_gradients(eng.finish(), 1.0 / world)
+        plan = StepPlan(exs[1], engs[1], grad_scale=1.0 / world, warmup=1, threads=threads)  # 1 eager step
+        st = plan.stats()
+        for _ in range(3):                      # ... + 3 native replays, P2P kernels included
+            plan.replay()
+            engs[1].poll_errors()
+        torch.cuda.synchronize()
+        for e in engs:
+            e.p2p.check()
+        a, b = exs
+        bitwise = all(torch.equal(x, y) for x, y in zip((a.P.master, a.P.momentum, a.P.bn_state, a.P.wbf16),
+                                                         (b.P.master, b.P.momentum, b.P.bn_state, b.P.wbf16)))
+        out = b.P.master.view(torch.int32).to(torch.int64).sum().reshape(1).cpu()
+        gathered = [torch.zeros_like(out) for _ in range(world)]
+        dist.all_gather(gathered, out)
+        same = all(torch.equal(gathered[0], t) for t in gathered)
+        q.put((rank, bitwise, same, st))
+        dist.barrier()
+        for e in engs:
+            e.close()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), False, None))
+
+
+@pytest.mark.parametrize("threads,wire,inline", [(1, "fp32", "1"), (2, "bf16", "0"), (1, "fp32", "0")])
+def test_plan_replay_dp_p2p_step_bitwise_equals_eager(threads, wire, inline):
+    """the P2P data-parallel step (step-boundary kernel, bf16 wire casts, every
+    bucket's reduce on the P2P comm stream behind its readiness events, the update reading the
+    exchange's error word) recorded into ONE native plan segment and replayed is bitwise identical
+    to the eager DP+P2P step, on two ranks sharing cuda:0 (deterministic mode); the reductions
+    inline on the compute stream (the default for small gradients) or on the comm stream."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_plan_p2p_worker, args=(r, 2, port, q, threads, wire, inline)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, bitwise, same, st in res:
+        assert bitwise is True, (rank, bitwise)
+        assert same
+        assert st["segments"] == 1, st   # one native segment: no host-issued collectives
+
+
+@pytest.mark.timeout(420)
+def test_bench_multirank_p2p_plan_path_one_device():
+    """bench.py at world 2 with the P2P all-reduce replayed as a native plan (--allreduce p2p
+    --plan 1 --graph 0): replicas end bit-identical."""
+    r = _bench_two_ranks(["--dataset", "cifar10", "--resnet_size", "20", "--bucket_mb", "0.05",
+                          "--allreduce", "p2p", "--plan", "1", "--graph", "0"])
+    dp = r["data_parallel"]
+    assert r["n_gpus"] == 2 and dp["allreduce"] == "p2p", r
+    assert r["config"]["step_mode"].startswith("plan"), r["config"]
+    assert dp["replicas_in_sync"] is True, dp
+    assert r["value"] > 0 and r["final_loss"] == r["final_loss"]
 
 
 def _schedule_worker(backend, port, q):

@@ -35,9 +35,11 @@ def test_graph_step_side_stream_trial(monkeypatch, trial):
         assert sess.side_choice is None and sess.ex.side is not None
 
 
-def test_p2p_dp_graph_step_side_stream_trial(monkeypatch):
-    """The same trial on the data-parallel step with the P2P all-reduce (single-rank engine,
-    whole step incl. the reductions in one graph): both candidates train, the global step counts
+def test_p2p_dp_session_step_mode_and_side_stream_trials(monkeypatch):
+    """The data-parallel step with the P2P all-reduce (single-rank engine): its first steps time
+    the whole-step graph (reductions included) against the native plans with the P2P kernels
+    recorded (runtime/plan.py; with and without the side stream) and keep the fastest; a kept
+    graph continues with its side-stream trial. Every candidate trains, the global step counts
     every real step, the P2P error word stays clear."""
     monkeypatch.setenv("DRN_SIDE_TRIAL", "1")
     monkeypatch.setenv("DRN_FORCE_DP", "1")
@@ -52,12 +54,20 @@ def test_p2p_dp_graph_step_side_stream_trial(monkeypatch):
     try:
         sess = TrainingSession(cifar_resnet_v2(8), 16, ClusterInfo(device="cuda:0"), weight_decay=2e-4,
                                lr_schedule=lr_mod.for_dataset("cifar10"), use_graph=True, allreduce="p2p")
-        assert sess.use_graph and sess.engine is not None and sess.engine.p2p is not None
-        sess.run(SyntheticFeeder(sess.ex, seed=0), [StopAtStepHook(50)])
+        assert not sess.use_graph and sess._trial is not None
+        assert sess.engine is not None and sess.engine.p2p is not None
+        sess.run(SyntheticFeeder(sess.ex, seed=0), [StopAtStepHook(100)])
         torch.cuda.synchronize()
-        assert sess.global_step == 50 and sess.failed is None   # (run() polled the error word every step)
-        c = sess.side_choice
-        assert c is not None and c["side_ms"] > 0 and c["one_stream_ms"] > 0, c
+        assert sess.global_step == 100 and sess.failed is None   # (run() polled the error word every step)
+        c = sess.graph_choice
+        assert c is not None and c["graph_ms"] > 0 and c["plan_ms"] > 0 and c["plan_one_stream_ms"] > 0, c
+        if c["mode"] == "graph":
+            assert sess.use_graph and sess._plan is None
+            s = sess.side_choice
+            assert s is not None and s["side_ms"] > 0 and s["one_stream_ms"] > 0, s
+        else:
+            assert c["mode"] in ("native plan", "native plan (one stream)"), c
+            assert not sess.use_graph and sess._plan is not None and sess._plan.p2p is not None
         assert float(sess.ex.metrics()["cross_entropy"]) == float(sess.ex.metrics()["cross_entropy"])
     finally:
         if dist.is_initialized():
