@@ -344,6 +344,7 @@ def main():
                        "image_size": spec.image_size, "num_classes": spec.num_classes,
                        "parallelism": f"dp{world}", "hip_graph": bool(use_graph), "step_mode": mode,
                        "wgrad_side_stream": ex.side is not None and mode not in one_stream,
+                       "fused_stem_pool": bool(getattr(ex, "stem_pool", False)),
                        "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")},
             "final_loss": round(loss, 4),
             "host_enqueue_ms": round(t_host, 3),

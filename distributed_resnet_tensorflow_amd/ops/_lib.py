@@ -114,6 +114,7 @@ _SIGS = {
     "drn_stem_pack_input": ([c_p, c_p, c_int, c_int, c_p], c_int),
     "drn_stem_pack_weights": ([c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p], c_int),
     "drn_stem_unpack_grad": ([c_p, c_p, c_int, c_int, c_int, c_int, c_int, c_int, c_p], c_int),
+    "drn_stem_conv_pool": ([c_p, c_p, c_p, c_p, c_p] + [c_int] * 11 + [c_p], c_int),
     "drn_weight_tflip": ([c_p, c_p, c_p, c_int, c_i64, c_p], c_int),
     "drn_fill_f32": ([c_p, c_i64, c_f, c_p], c_int),
     "drn_cifar_augment": ([c_p, c_p, c_p, c_int, c_int, c_int, c_int, c_p], c_int),

@@ -884,6 +884,18 @@ class HipBackend(_Common):
         _lib.check(self.L.drn_stem_pack_weights(w.data_ptr(), wp.data_ptr(), K, R, S, C, S8, C4, self.stream()),
                    "drn_stem_pack_weights")
 
+    def stem_conv_pool(self, xp, w4, y, arg, g, H, W, P, Q, stats=None):
+        """Fused packed stem conv (xp [N,H,W+2,4], w4 [K,7,8,4], geometry g of the packed conv)
+        + 3x3/2 max-pool into y / arg [N,ceil(P/2),ceil(Q/2),K]; stats (optional [R][2][K] fp32):
+        += per-channel (sum, sumsq) of y (csrc/kernels/stem_pool.hip stem_conv_pool_kernel)."""
+        N, PP, QP, K = y.shape
+        assert tuple(xp.shape) == (N, H, W + 2, 4) and tuple(w4.shape) == (K, 7, 8, 4) and g.stride == 2
+        assert arg.shape == y.shape and xp.is_contiguous() and w4.is_contiguous() and y.is_contiguous()
+        rep = stats.numel() // (2 * K) if stats is not None else 0
+        _lib.check(self.L.drn_stem_conv_pool(xp.data_ptr(), w4.data_ptr(), y.data_ptr(), arg.data_ptr(), _ptr(stats),
+                                             rep, N, H, W, P, Q, PP, QP, K, g.pad_h, g.pad_w, self.stream()),
+                   "drn_stem_conv_pool")
+
     def stem_unpack_grad(self, dwp, dw):
         K, R, S, C = dw.shape
         K2, R2, S8, C4 = dwp.shape

@@ -357,6 +357,12 @@ class Executor:
             self.stem_geom4 = ConvGeom(g0.stride, g0.pad_h, g0.pad_w - 1, 1)
         self.labels = torch.zeros(N, dtype=torch.int32, device=self.device)
         hs = sp.stem_hw
+        # fused stem conv + max-pool (DRN_STEM_POOL=0: the conv and pooling kernels separately):
+        # the ImageNet stem geometry (7x7/2 packed, 3x3/2 pool without leading pad)
+        self.stem_pool = (self.stem_pack and sp.maxpool and c0.k == 7 and hs % 16 == 0 and hs <= 112
+                          and c0.cout % 32 == 0 and sp.pool_hw == (hs + 1) // 2
+                          and max((sp.pool_hw - 1) * 2 + 3 - hs, 0) // 2 == 0 and 0 <= self.stem_geom4.pad_w <= 2 and self.stem_geom4.pad_h <= 3
+                          and os.environ.get("DRN_STEM_POOL", "1") == "1")
         self.stem_out = self._act(N, hs, hs, sp.stem.cout)
         max_act = N * hs * hs * sp.stem.cout
         max_bn_part = 0
@@ -566,13 +572,23 @@ class Executor:
         if train:
             be.zero_(self.stats_arena)
         st = self.stem_op
-        if self.stem_pack:
+        if self.stem_pool:
+            # conv + max-pool + the pooled BN statistics in one kernel: the conv output never
+            # reaches HBM (csrc/kernels/stem_pool.hip stem_conv_pool_kernel)
+            be.stem_pack_input(self.images, self.stem_xp)
+            fused = train and not self.deterministic
+            img = sp.image_size
+            be.stem_conv_pool(self.stem_xp, self.stem_w4, self.pool_out, self.pool_arg, self.stem_geom4, img, img,
+                              sp.stem_hw, sp.stem_hw, stats=self.pool_stats if fused else None)
+            if train and not fused:
+                be.bn_stats(self.pool_out, self.pool_stats)
+        elif self.stem_pack:
             be.stem_pack_input(self.images, self.stem_xp)
             be.conv_fwd(self.stem_xp, self.stem_w4, self.stem_out, self.stem_geom4,
                         stats=self.stem_stats if train else None)
         else:
             be.conv_fwd(self.images, st.w, self.stem_out, st.geom, stats=self.stem_stats if train else None)
-        if sp.maxpool:
+        if sp.maxpool and not self.stem_pool:
             ph = sp.pool_hw
             pad = max((ph - 1) * 2 + 3 - sp.stem_hw, 0) // 2
             # the first block's BN statistics come out of the pooling kernel itself (the

@@ -974,6 +974,67 @@ def test_wgrad_atomic_split_k(hip, ref, case, ns):
     assert rel(dw, dw_ref) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,pad", [(2, 224, 3), (3, 64, 3), (2, 96, 3)])
+def test_fused_stem_conv_pool(hip, ref, N, H, pad):
+    """Fused ImageNet stem (csrc/kernels/stem_pool.hip stem_conv_pool_kernel): packed 7x7/2 conv +
+    3x3/2 max-pool + the pooled BN statistics in one kernel equals the two-kernel path (packed conv
+    with the tuned configuration, then maxpool_fwd) -- pooled values, first-max taps, statistics --
+    and the fp32 reference (conv, bf16 rounding, ceil-mode 3x3/2 max-pool)."""
+    import torch.nn.functional as F
+    torch.manual_seed(H + N)
+    K, R = 64, 7
+    # pad 3: the reference's conv2d_fixed_padding (explicit 3 + 3, what the executor runs)
+    P = (H + 2 * pad - R) // 2 + 1
+    PP = (P + 1) // 2
+    x = torch.zeros(N, H, H, 8)
+    x[..., :3] = torch.randn(N, H, H, 3)
+    x = bf(x)
+    w = torch.zeros(K, R, R, 8)
+    w[..., :3] = torch.randn(K, R, R, 3) * (2.0 / (R * R * 3)) ** 0.5
+    w = bf(w)
+    n_xp = N * H * (H + 2) * 4
+    buf = torch.zeros(n_xp + 64, dtype=torch.bfloat16, device="cuda")
+    xp = buf[:n_xp].view(N, H, H + 2, 4)
+    hip.stem_pack_input(x.cuda(), xp)
+    w4 = torch.zeros(K, R, 8, 4, dtype=torch.bfloat16, device="cuda")
+    hip.stem_pack_weights(w.cuda(), w4)
+    g4 = ConvGeom(stride=2, pad_h=pad, pad_w=pad - 1)
+    # two-kernel path
+    y = torch.zeros(N, P, P, K, dtype=torch.bfloat16, device="cuda")
+    hip.conv_fwd(xp, w4, y, g4)
+    yp_ref = torch.zeros(N, PP, PP, K, dtype=torch.bfloat16, device="cuda")
+    arg_ref = torch.zeros(N, PP, PP, K, dtype=torch.uint8, device="cuda")
+    st_ref = torch.zeros(2, 2, K, device="cuda")
+    hip.maxpool_fwd(y, yp_ref, arg_ref, 3, 2, 0, 0, stats=st_ref)
+    # fused
+    yp = torch.full((N, PP, PP, K), float("nan"), dtype=torch.bfloat16, device="cuda")
+    arg = torch.full((N, PP, PP, K), 77, dtype=torch.uint8, device="cuda")
+    st = torch.zeros(3, 2, K, device="cuda")
+    hip.stem_conv_pool(xp, w4, yp, arg, g4, H, H, P, P, stats=st)
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(yp.float()).all())
+    diff = (yp.float() - yp_ref.float()).abs()
+    # same bf16 conv outputs up to the MFMA summation order: nearly all pooled values identical
+    assert (diff > 0).float().mean().item() < 1e-3, (diff > 0).float().mean().item()
+    assert diff.max().item() <= 0.05 * yp_ref.float().abs().max().item()
+    same = diff == 0
+    assert (arg[same] == arg_ref[same]).float().mean().item() > 0.999
+    assert int(arg.max()) <= 8
+    s1, s0 = st.sum(0).view(-1).cpu(), st_ref.sum(0).view(-1).cpu()
+    assert rel(s1[:K], s0[:K]) < 1e-3 and rel(s1[K:], s0[K:]) < 1e-3
+    # the fp32 reference
+    y32 = torch.zeros(N, P, P, K)
+    ref.conv_fwd(x.float(), w.float(), y32, ConvGeom(stride=2, pad_h=pad, pad_w=pad))
+    yb = bf(y32).float().permute(0, 3, 1, 2)
+    p32 = F.max_pool2d(yb, 3, 2, ceil_mode=True).permute(0, 2, 3, 1)
+    assert tuple(p32.shape) == (N, PP, PP, K)
+    assert rel(yp.float().cpu(), p32) < 1e-2
+    # refused geometry: output width not a multiple of 16
+    a_bad = hip.L.drn_stem_conv_pool(xp.data_ptr(), w4.data_ptr(), yp.data_ptr(), arg.data_ptr(), None, 1, N, H, H,
+                                     P, P - 8, PP, (P - 8 + 1) // 2, K, pad, 1, hip.stream())
+    assert a_bad != 0
+
+
 @pytest.mark.parametrize("N,H", [(2, 16), (3, 30), (2, 224)])
 def test_packed_stem(hip, ref, N, H):
     """Packed stem (csrc/kernels/stem.hip): the 7x7/2 conv over a 4-channel, column-padded copy of
