@@ -202,6 +202,9 @@ class Executor:
         # largest BN input is 128x32x32x16 = 2.1M). 3M: the ImageNet 7x7x512 stage (3.2M at bs128)
         # is materialised -- its 3x3 conv and weight gradient ran 80 / 77 us with the prologue
         self.mat_min_elems = 3_000_000
+        # the stem's max-pool backward on the weight-gradient side stream in deferred-tail steps
+        # (DRN_POOL_BWD_SIDE=0: on the main stream before the optimizer)
+        self.pool_bwd_side = os.environ.get("DRN_POOL_BWD_SIDE", "1") == "1"
         self.fdt = backend.acc_dtype
         self.P = params or ParamStore(spec, self.device, keep_bf16=self.is_hip, seed=seed, dtype=self.fdt)
         self.grad_ready: Optional[Callable[[int], None]] = None
@@ -713,28 +716,38 @@ class Executor:
             self._report(bp.grad_lo)
         d_x0 = self._view(bufs[cur], self.blocks[0].x)
         st = self.stem_op
+        deferred = defer_tail and self.side is not None and self.grad_ready is None and self._stem_hi > 0
+        pool_bwd = None
         if sp.maxpool:
             k = self._take(bufs, (cur,))
             d_stem = self._view(bufs[k], self.stem_out)
             self._claim(bufs[k])
             ph = sp.pool_hw
             pad = max((ph - 1) * 2 + 3 - sp.stem_hw, 0) // 2
-            be.maxpool_bwd(d_x0, self.pool_arg, d_stem, 3, 2, pad, pad)
+
+            def pool_bwd():
+                be.maxpool_bwd(d_x0, self.pool_arg, d_stem, 3, 2, pad, pad)
+            if not (deferred and self.pool_bwd_side):
+                pool_bwd()
+                pool_bwd = None
         else:
             d_stem = d_x0
         self._tail_ev = None
-        if defer_tail and self.side is not None and self.grad_ready is None and self._stem_hi > 0:
+        if deferred:
             # every weight gradient but the stem's is issued on the side stream: the optimizer
             # may update those while the stem's weight gradient (the last, ~0.2 ms on ImageNet)
-            # still runs -- see apply_gradients
+            # still runs -- see apply_gradients. With pool_bwd_side the max-pool backward that
+            # produces the stem's output gradient runs there too, ahead of it: the optimizer
+            # then starts right after the last BatchNorm backward instead of after the pooling's
+            # (all three are HBM-bound and share the tail)
             self._tail_ev = self.sched.record(self.side)
         if self.stem_pack:
             if getattr(be, "wgrad_atomic_used", False):
                 be.zero_(self.stem_dw4)
-            self._wgrad(self.stem_xp, d_stem, self.stem_dw4, self.stem_geom4,
+            self._wgrad(self.stem_xp, d_stem, self.stem_dw4, self.stem_geom4, pre=pool_bwd,
                         post=lambda: be.stem_unpack_grad(self.stem_dw4, st.dw))
         else:
-            self._wgrad(self.images, d_stem, st.dw, st.geom)
+            self._wgrad(self.images, d_stem, st.dw, st.geom, pre=pool_bwd)
         if self._tail_ev is not None:
             self._stem_ev = self.sched.record(self.side)
         self._report(0)
@@ -776,10 +789,13 @@ class Executor:
         self._reported = True
 
     # -- weight gradients on the side stream ---------------------------------------------------------
-    def _wgrad(self, x, dy, dw, geom, in_bn=None, dy_buf=None, post=None):
-        """Weight gradient into dw (on the side stream when enabled); post() runs right after it,
-        on the same stream (the packed stem maps its gradient back to the checkpoint layout)."""
+    def _wgrad(self, x, dy, dw, geom, in_bn=None, dy_buf=None, post=None, pre=None):
+        """Weight gradient into dw (on the side stream when enabled); pre() / post() run right
+        before / after it, on the same stream (the stem's max-pool backward producing dy; the
+        packed stem mapping its gradient back to the checkpoint layout)."""
         if self.side is None:
+            if pre is not None:
+                pre()
             self.be.conv_wgrad(x, dy, dw, geom, in_bn=in_bn, ws=self.wgrad_ws)
             if post is not None:
                 post()
@@ -787,6 +803,8 @@ class Executor:
         main = torch.cuda.current_stream(self.device)
         self.sched.wait_stream(self.side, main)          # x and dy are complete
         with torch.cuda.stream(self.side):
+            if pre is not None:
+                pre()
             self.be.conv_wgrad(x, dy, dw, geom, in_bn=in_bn, ws=self.wgrad_ws)
             if post is not None:
                 post()
