@@ -205,6 +205,11 @@ class Executor:
         # the stem's max-pool backward on the weight-gradient side stream in deferred-tail steps
         # (DRN_POOL_BWD_SIDE=0: on the main stream before the optimizer)
         self.pool_bwd_side = os.environ.get("DRN_POOL_BWD_SIDE", "1") == "1"
+        # ... and the optimizer's update of every block but the first starts as soon as the side
+        # stream has finished their weight gradients (DRN_EARLY_SGD): on the main stream, in the
+        # window where it otherwise idles waiting for the first block's weight gradients
+        self.early_sgd = os.environ.get("DRN_EARLY_SGD", "1") == "1"
+        self._pre_ev, self._pre_lo = None, 0
         self.fdt = backend.acc_dtype
         self.P = params or ParamStore(spec, self.device, keep_bf16=self.is_hip, seed=seed, dtype=self.fdt)
         self.grad_ready: Optional[Callable[[int], None]] = None
@@ -709,14 +714,19 @@ class Executor:
             if not (self.is_hip and torch.cuda.is_current_stream_capturing()):
                 self.sched.wait(torch.cuda.current_stream(self.device), self._tflip_ev, key="tflip")
             self._tflip_ev = None
+        deferred = defer_tail and self.side is not None and self.grad_ready is None and self._stem_hi > 0
+        self._pre_ev = None
         for bp in reversed(self.blocks):
+            if deferred and self.early_sgd and bp is self.blocks[0] and len(self.blocks) > 1:
+                # every gradient at offsets >= the next block's is complete once the side stream
+                # gets here: the optimizer may update those while block 0 finishes (apply_gradients)
+                self._pre_ev, self._pre_lo = self.sched.record(self.side), self.blocks[1].grad_lo
             cur = self._block_bwd(bp, bufs, cur)
             if self.check_nan:
                 self._check(self._view(bufs[cur], bp.x), f"input gradient of block {bp.blk.stage}.{bp.blk.index}")
             self._report(bp.grad_lo)
         d_x0 = self._view(bufs[cur], self.blocks[0].x)
         st = self.stem_op
-        deferred = defer_tail and self.side is not None and self.grad_ready is None and self._stem_hi > 0
         pool_bwd = None
         if sp.maxpool:
             k = self._take(bufs, (cur,))
@@ -935,10 +945,24 @@ class Executor:
             # parameters [stem_hi, end) while the stem's weight gradient finishes on the side
             # stream (the stem has no data-gradient weights, so the refresh goes first too)
             hi, ev = self._stem_hi, self._tail_ev
-            self.sched.wait(torch.cuda.current_stream(self.device), ev)
-            wb = P.wbf16[hi:] if P.wbf16 is not None else None
-            self.be.sgd_momentum(P.master[hi:], P.momentum[hi:], g[hi:], wb, self.lr_t, self.mom, self.wd,
-                                 grad_scale, skip)
+            main = torch.cuda.current_stream(self.device)
+            if self._pre_ev is not None and self._pre_lo > hi:
+                lo, pre = self._pre_lo, self._pre_ev
+                self._pre_ev = None
+                self.sched.wait(main, pre)
+                wb = P.wbf16[lo:] if P.wbf16 is not None else None
+                self.be.sgd_momentum(P.master[lo:], P.momentum[lo:], g[lo:], wb, self.lr_t, self.mom, self.wd,
+                                     grad_scale, skip)
+                self.sched.wait(main, ev)
+                wb = P.wbf16[hi:lo] if P.wbf16 is not None else None
+                self.be.sgd_momentum(P.master[hi:lo], P.momentum[hi:lo], g[hi:lo], wb, self.lr_t, self.mom,
+                                     self.wd, grad_scale, skip)
+            else:
+                self._pre_ev = None
+                self.sched.wait(main, ev)
+                wb = P.wbf16[hi:] if P.wbf16 is not None else None
+                self.be.sgd_momentum(P.master[hi:], P.momentum[hi:], g[hi:], wb, self.lr_t, self.mom, self.wd,
+                                     grad_scale, skip)
             self.refresh_dgrad_weights(stem=False)  # (the stem's weights are not updated yet)
             self.join_grads()
             wb = P.wbf16[:hi] if P.wbf16 is not None else None
