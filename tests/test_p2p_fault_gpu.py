@@ -56,7 +56,8 @@ def _worker(rank, mode, port, ck, q, stop):
         cluster = ClusterInfo(rank=rank, world=2, device="cuda:0", backend="gloo")
         sess = TrainingSession(cifar_resnet_v2(8), 8, cluster, weight_decay=2e-4,
                                lr_schedule=lr_mod.for_dataset("cifar10"), checkpoint_dir=ck if rank == 0 else "",
-                               use_graph=(mode == "stall"), allreduce="p2p", bucket_mb=0.05)
+                               use_graph=(mode == "stall"), allreduce="p2p", bucket_mb=0.05,
+                               step_trial=False)   # (stall: the whole-step graph, no mode trial)
         assert sess.engine.p2p is not None and len(sess.engine.buckets) > 1
         assert sess.use_graph == (mode == "stall")
         feeder = SyntheticFeeder(sess.ex, seed=rank)
