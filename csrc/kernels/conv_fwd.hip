@@ -733,7 +733,12 @@ __global__ __launch_bounds__(NW * 64) void conv_fwd_glds_sk_kernel(DrnConvFwdArg
     const unsigned t0 = u - tbase, t1 = (tend < uend ? tend : uend) - tbase;  // (uniform)
     const unsigned bf = __builtin_amdgcn_readfirstlane(owner(tbase));
     const unsigned bl = __builtin_amdgcn_readfirstlane(owner(tend - 1));
-    if (!first) __syncthreads();  // the previous segment's LDS use is over
+    if (!first) {
+      __syncthreads();  // the previous segment's LDS use is over
+      // a consumer-side BN finalize publishes (and moves the moving averages) once: in the
+      // first segment of workgroup 0, not again if that workgroup's range spans several tiles
+      if constexpr (PRO) a.in_fin.publish = 0;
+    }
     // (no epilogue-operand prefetch: most segments end in a partial tile, not an epilogue)
     conv_fwd_glds_tile<BP, BC, WAVES_P, NS, NW, false, BK, PRO, false, NH, true, IL>(
         a, zero, smem, (int)tile, (int)(bl - bf + 1), (int)(b - bf), a.ksplit, (int)t0, (int)(t1 - t0));

@@ -1,0 +1,20 @@
+# round-6 GPU call 34: publish-once BN finalize (one finalizing workgroup per large publishing
+# launch, DRN_FIN_ONCE): GPU tests, bench A/B (3 rounds), remaining standalone finalize launches
+set -o pipefail
+ROOT=$(pwd)
+O=$ROOT/gpurun_out/r6
+mkdir -p $O
+export PYTHONPATH=$ROOT
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_ops_gpu.py tests/test_executor_gpu.py \
+  tests/test_plan_gpu.py tests/test_bench_geometry_gpu.py > $O/c34_tests.txt 2>&1 || { tail -40 $O/c34_tests.txt; exit 1; }
+tail -1 $O/c34_tests.txt
+for i in 1 2 3; do
+  timeout -k 10 200 python bench.py > $O/c34_x.json 2>> $O/c34.err || { tail $O/c34.err; exit 1; }
+  echo "once $(grep -o '"ms_per_step": [0-9.]*\|"step_mode": "[a-z_]*"' $O/c34_x.json | tr '\n' ' ')" | tee -a $O/c34_ab.txt
+  DRN_FIN_ONCE=0 timeout -k 10 200 python bench.py > $O/c34_x.json 2>> $O/c34.err || { tail $O/c34.err; exit 1; }
+  echo "launch $(grep -o '"ms_per_step": [0-9.]*\|"step_mode": "[a-z_]*"' $O/c34_x.json | tr '\n' ' ')" | tee -a $O/c34_ab.txt
+done
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/c34_prof -o p --output-format csv -- \
+  python3 $ROOT/bench.py --steps 10 --warmup 3 > $O/c34_prof.log 2>&1 || { tail -20 $O/c34_prof.log; exit 1; }
+grep -i "fin_fwd\|finalize" $O/c34_prof/p_kernel_stats.csv | cut -c1-120

@@ -222,6 +222,44 @@ def test_conv_fwd_streamk(hip, ref, case, cfg, G):
     assert int(hip.ks_tickets.abs().sum()) == 0
 
 
+@pytest.mark.parametrize("G", [2, 3])
+def test_conv_fwd_streamk_prologue_finalize_publishes_once(hip, G):
+    """A stream-K launch whose workgroups each walk several tiles (G < tiles) with a publishing
+    consumer-side BN finalize in the prologue: the moving averages move ONCE (workgroup 0's first
+    segment), the output equals the conv reading separately finalized scale / shift."""
+    from distributed_resnet_tensorflow_amd.ops.backend import BnCfin
+    torch.manual_seed(13)
+    N, H, C, K = 2, 14, 128, 256
+    x = bf(torch.randn(N, H, H, C) + 0.2).cuda()
+    wgt = bf(torch.randn(K, 1, 1, C) * 0.05).cuda()
+    gamma, beta = (torch.rand(C) + 0.5).cuda(), (torch.randn(C) * 0.2).cuda()
+    xf = x.float().reshape(-1, C)
+    M = xf.shape[0]
+    st = (torch.stack([xf.sum(0), (xf * xf).sum(0)]).unsqueeze(0) / 4).repeat(4, 1, 1).contiguous()
+    sc0, sh0, mu0, is0 = (torch.zeros(C, device="cuda") for _ in range(4))
+    hip.bn_finalize(st, 4, M, gamma, beta, None, None, sc0, sh0, mu0, is0, 0.997, 1e-5, update_running=False)
+    g = ConvGeom(1, 0, 0)
+    want = torch.empty(N, H, H, K, dtype=torch.bfloat16, device="cuda")
+    hip.conv_fwd(x, wgt, want, g, in_bn=(sc0, sh0))
+    for cfg in KS:
+        rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+        sc, sh, mu, isd = (torch.full((C,), 7.0, device="cuda") for _ in range(4))
+        fin = BnCfin(st, float(M), gamma, beta=beta, run_mean=rm, run_var=rv, scale=sc, shift=sh, mean=mu,
+                     invstd=isd, publish=True)
+        got = torch.empty_like(want)
+        a = hip.conv_args(x, wgt, got, g, in_bn=(sc, sh), in_fin=fin)
+        a.cfg = cfg
+        if hip.L.drn_conv_sk_slots_cfg(ctypes.byref(a), cfg, G) == 0:
+            continue
+        hip._set_ksplit(a, -G)
+        assert hip.L.drn_conv_fwd2(ctypes.byref(a), hip.zero_page.data_ptr(), hip.stream()) == 0, cfg
+        torch.cuda.synchronize()
+        assert rel(got, want) < 1e-2, cfg
+        assert rel(rm, 0.003 * mu0) < 1e-4, cfg  # one update from 0, not two
+        assert rel(sc, sc0) < 1e-5, cfg
+    assert int(hip.ks_tickets.abs().sum()) == 0
+
+
 @pytest.mark.parametrize("cfg", [0, 13, 31])
 def test_conv_splitk_handoff_stress(hip, ref, cfg):
     """The in-launch partial-tile hand-off under hostile cache state: before every launch the
